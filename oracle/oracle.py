@@ -1,0 +1,272 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes loader for the CPU oracle (oracle/liboracle.so) and, when built,
+the reference sw/ encoder compiled in place (oracle/_ref/libgcow_ref.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module; the product
+package gcow_amd/ never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+F32, BF16 = 3, 5
+
+
+class Params(C.Structure):
+    _fields_ = [("minbits", C.c_uint), ("maxbits", C.c_uint), ("maxprec", C.c_uint), ("minexp", C.c_int)]
+
+    def tuple(self):
+        return (self.minbits, self.maxbits, self.maxprec, self.minexp)
+
+    def __repr__(self):
+        return "Params(%d, %d, %d, %d)" % self.tuple()
+
+
+_lib = None
+_ref = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        P = C.POINTER
+        L.orc_block_exponent.restype = C.c_int
+        L.orc_block_exponent.argtypes = [P(C.c_float), C.c_uint]
+        L.orc_fwd_cast.argtypes = [P(C.c_int32), P(C.c_float), C.c_uint, C.c_int]
+        L.orc_fwd_xform.argtypes = [P(C.c_int32), C.c_uint]
+        L.orc_inv_xform.argtypes = [P(C.c_int32), C.c_uint]
+        L.orc_fwd_reorder.argtypes = [P(C.c_uint32), P(C.c_int32), C.c_uint]
+        L.orc_perm.restype = P(C.c_ubyte)
+        L.orc_perm.argtypes = [C.c_uint]
+        L.orc_encode_ints.restype = C.c_uint
+        L.orc_encode_ints.argtypes = [P(C.c_uint64), P(C.c_uint64), P(C.c_uint32), C.c_uint, C.c_uint, C.c_uint]
+        L.orc_encode_iblock.restype = C.c_uint
+        L.orc_encode_iblock.argtypes = [P(C.c_uint64), P(C.c_uint64), C.c_uint, C.c_uint, C.c_uint, P(C.c_int32),
+                                        C.c_uint]
+        L.orc_encode_fblock.restype = C.c_uint
+        L.orc_encode_fblock.argtypes = [P(C.c_uint64), P(C.c_uint64), P(Params), P(C.c_float), C.c_uint]
+        L.orc_gather_block.argtypes = [P(C.c_float), C.c_void_p, C.c_int, C.c_uint, P(C.c_size_t),
+                                       P(C.c_ssize_t), P(C.c_size_t)]
+        L.orc_precision.restype = C.c_uint
+        L.orc_precision.argtypes = [C.c_int, C.c_uint, C.c_int, C.c_uint]
+        L.orc_num_blocks.restype = C.c_size_t
+        L.orc_num_blocks.argtypes = [C.c_uint, P(C.c_size_t)]
+        L.orc_compress.restype = C.c_uint64
+        L.orc_compress.argtypes = [C.c_void_p, C.c_int, C.c_uint, P(C.c_size_t), P(C.c_ssize_t), P(Params),
+                                   P(C.c_uint64), C.c_size_t]
+        L.orc_compress_mt.restype = C.c_uint64
+        L.orc_compress_mt.argtypes = L.orc_compress.argtypes + [C.c_int]
+        L.orc_block_bits.argtypes = [C.c_void_p, C.c_int, C.c_uint, P(C.c_size_t), P(C.c_ssize_t), P(Params),
+                                     P(C.c_uint32)]
+        L.orc_decompress.restype = C.c_uint64
+        L.orc_decompress.argtypes = [P(C.c_float), C.c_uint, P(C.c_size_t), P(C.c_ssize_t), P(Params),
+                                     P(C.c_uint64), C.c_size_t]
+        for f in ("orc_set_accuracy",):
+            getattr(L, f).argtypes = [P(Params), C.c_double]
+        L.orc_set_rate.argtypes = [P(Params), C.c_double, C.c_uint]
+        L.orc_set_precision.argtypes = [P(Params), C.c_uint]
+        L.orc_gen_bump2d.argtypes = [P(C.c_float), C.c_size_t, C.c_int]
+        L.orc_gen_normal.argtypes = [P(C.c_float), C.c_size_t, C.c_double, C.c_uint64, C.c_int]
+        _lib = L
+    return _lib
+
+
+def ref():
+    """Reference sw/ encoder (2-D only) compiled from /root/reference sources, or None if not built."""
+    global _ref
+    if _ref is None:
+        path = os.path.join(HERE, "_ref", "libgcow_ref.so")
+        if not os.path.exists(path):
+            return None
+        L = C.CDLL(path)
+        P = C.POINTER
+        L.gcow_ref_compress_2d.restype = C.c_size_t
+        L.gcow_ref_compress_2d.argtypes = [P(C.c_float), C.c_size_t, C.c_size_t, C.c_uint, C.c_uint, C.c_uint,
+                                           C.c_int, P(C.c_uint64), C.c_size_t]
+        L.gcow_ref_set_accuracy.restype = C.c_double
+        L.gcow_ref_set_accuracy.argtypes = [C.c_double, P(C.c_uint), P(C.c_uint), P(C.c_uint), P(C.c_int)]
+        L.gcow_ref_block_exponent.restype = C.c_int
+        L.gcow_ref_block_exponent.argtypes = [P(C.c_float), C.c_uint]
+        L.gcow_ref_fwd_cast.argtypes = [P(C.c_int32), P(C.c_float), C.c_uint, C.c_int]
+        L.gcow_ref_fwd_decorrelate_2d.argtypes = [P(C.c_int32)]
+        L.gcow_ref_fwd_reorder_2d.argtypes = [P(C.c_uint32), P(C.c_int32)]
+        L.gcow_ref_encode_iblock.restype = C.c_uint
+        L.gcow_ref_encode_iblock.argtypes = [P(C.c_uint64), C.c_size_t, C.c_uint, C.c_uint, C.c_uint, C.c_uint,
+                                             P(C.c_int32), P(C.c_uint64)]
+        _ref = L
+    return _ref
+
+
+def _p(a, ct):
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+# ------------------------------------------------------------------ parameter helpers
+def accuracy(tol: float) -> Params:
+    p = Params()
+    lib().orc_set_accuracy(C.byref(p), tol)
+    return p
+
+
+def rate(r: float, dims: int) -> Params:
+    p = Params()
+    lib().orc_set_rate(C.byref(p), r, dims)
+    return p
+
+
+def precision(prec: int) -> Params:
+    p = Params()
+    lib().orc_set_precision(C.byref(p), prec)
+    return p
+
+
+def expert(minbits, maxbits, maxprec, minexp) -> Params:
+    return Params(minbits, maxbits, maxprec, minexp)
+
+
+# ------------------------------------------------------------------ array API
+def _shape(shape):
+    """shape given numpy-style (slowest first); oracle wants (nx, ny, nz) fastest first."""
+    dims = len(shape)
+    n = (C.c_size_t * 3)(*(list(reversed(shape)) + [0] * (3 - dims)))
+    return dims, n
+
+
+def max_words(shape, p: Params) -> int:
+    dims = len(shape)
+    nb = 1
+    for s in shape:
+        nb *= (s + 3) // 4
+    size = 4 ** dims
+    mb = 9 + size - 1 + size * min(p.maxprec, 32)
+    if p.maxbits >= 9:
+        mb = min(mb, p.maxbits)
+    mb = max(mb, p.minbits)
+    return (nb * mb + 63) // 64 + 2
+
+
+def compress(arr: np.ndarray, p: Params, threads: int = 0):
+    """Encode a C-contiguous float32 (or bf16-as-uint16) array. Returns (words[uint64], total_bits)."""
+    arr = np.ascontiguousarray(arr)
+    dtype = BF16 if arr.dtype == np.uint16 else F32
+    if dtype == F32:
+        assert arr.dtype == np.float32
+    dims, n = _shape(arr.shape)
+    nw = max_words(arr.shape, p)
+    out = np.zeros(nw, dtype=np.uint64)
+    L = lib()
+    if threads and threads > 1:
+        bits = L.orc_compress_mt(arr.ctypes.data, dtype, dims, n, None, C.byref(p), _p(out, C.c_uint64), nw,
+                                 threads)
+    else:
+        bits = L.orc_compress(arr.ctypes.data, dtype, dims, n, None, C.byref(p), _p(out, C.c_uint64), nw)
+    return out[: (bits + 63) // 64].copy(), int(bits)
+
+
+def block_bits(arr: np.ndarray, p: Params) -> np.ndarray:
+    arr = np.ascontiguousarray(arr)
+    dtype = BF16 if arr.dtype == np.uint16 else F32
+    dims, n = _shape(arr.shape)
+    nb = lib().orc_num_blocks(dims, n)
+    out = np.zeros(nb, dtype=np.uint32)
+    lib().orc_block_bits(arr.ctypes.data, dtype, dims, n, None, C.byref(p), _p(out, C.c_uint32))
+    return out
+
+
+def decompress(words: np.ndarray, shape, p: Params) -> np.ndarray:
+    dims, n = _shape(shape)
+    out = np.zeros(shape, dtype=np.float32)
+    w = np.ascontiguousarray(words, dtype=np.uint64)
+    w = np.concatenate([w, np.zeros(2, np.uint64)])
+    lib().orc_decompress(_p(out, C.c_float), dims, n, None, C.byref(p), _p(w, C.c_uint64), len(w))
+    return out
+
+
+def gen_bump2d(n: int, f32sum: bool = False) -> np.ndarray:
+    out = np.empty((n, n), dtype=np.float32)
+    lib().orc_gen_bump2d(_p(out, C.c_float), n, int(f32sum))
+    return out
+
+
+def gen_normal(count: int, sigma: float = 1e-3, seed: int = 0x67636F77, inject: bool = True) -> np.ndarray:
+    out = np.empty(count, dtype=np.float32)
+    lib().orc_gen_normal(_p(out, C.c_float), count, sigma, seed, int(inject))
+    return out
+
+
+# ------------------------------------------------------------------ stage API (known-answer tests)
+def block_exponent(block: np.ndarray) -> int:
+    b = np.ascontiguousarray(block, dtype=np.float32)
+    return lib().orc_block_exponent(_p(b, C.c_float), b.size)
+
+
+def fwd_cast(fblock: np.ndarray, emax: int) -> np.ndarray:
+    f = np.ascontiguousarray(fblock, dtype=np.float32)
+    q = np.zeros(f.size, dtype=np.int32)
+    lib().orc_fwd_cast(_p(q, C.c_int32), _p(f, C.c_float), f.size, emax)
+    return q
+
+
+def fwd_xform(iblock: np.ndarray, dims: int) -> np.ndarray:
+    q = np.array(iblock, dtype=np.int32)
+    lib().orc_fwd_xform(_p(q, C.c_int32), dims)
+    return q
+
+
+def inv_xform(iblock: np.ndarray, dims: int) -> np.ndarray:
+    q = np.array(iblock, dtype=np.int32)
+    lib().orc_inv_xform(_p(q, C.c_int32), dims)
+    return q
+
+
+def fwd_reorder(iblock: np.ndarray, dims: int) -> np.ndarray:
+    q = np.ascontiguousarray(iblock, dtype=np.int32)
+    u = np.zeros(q.size, dtype=np.uint32)
+    lib().orc_fwd_reorder(_p(u, C.c_uint32), _p(q, C.c_int32), dims)
+    return u
+
+
+def perm(dims: int) -> list:
+    P = lib().orc_perm(dims)
+    return [P[i] for i in range(4 ** dims)]
+
+
+def encode_ints(ublock: np.ndarray, maxbits: int, maxprec: int, pos0: int = 0, words: np.ndarray | None = None):
+    u = np.ascontiguousarray(ublock, dtype=np.uint32)
+    if words is None:
+        words = np.zeros(64, dtype=np.uint64)
+    pos = C.c_uint64(pos0)
+    bits = lib().orc_encode_ints(_p(words, C.c_uint64), C.byref(pos), _p(u, C.c_uint32), maxbits, maxprec, u.size)
+    return words, int(pos.value), int(bits)
+
+
+def encode_iblock(iblock: np.ndarray, minbits, maxbits, maxprec, dims, pos0=0, words=None):
+    q = np.array(iblock, dtype=np.int32)
+    if words is None:
+        words = np.zeros(512, dtype=np.uint64)
+    pos = C.c_uint64(pos0)
+    bits = lib().orc_encode_iblock(_p(words, C.c_uint64), C.byref(pos), minbits, maxbits, maxprec,
+                                   _p(q, C.c_int32), dims)
+    return words, int(pos.value), int(bits)
+
+
+def put_bits_header(words: np.ndarray, value: int, nbits: int, pos0: int = 0) -> int:
+    """Write a header field via the oracle's coder path (used by known-answer tests)."""
+    # encode the header as verbatim bits: set bits directly (LSB-first)
+    for i in range(nbits):
+        if (value >> i) & 1:
+            p = pos0 + i
+            words[p >> 6] |= np.uint64(1) << np.uint64(p & 63)
+    return pos0 + nbits

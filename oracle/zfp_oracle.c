@@ -1,0 +1,638 @@
+/*
+ * zfp_oracle.c -- TEST INFRASTRUCTURE ONLY. Not part of the product; never linked by libgcow.so.
+ *
+ * Clean-room CPU restatement of the gcow sw/ block codec, written from the per-block spec
+ * (SURVEY.md Appendix A), each function citing the reference file:line it restates.
+ * Extended from sw/'s 2-D-only driver to d = 1, 2, 3 following LLNL zfp 0.5.5 (which sw/ is
+ * byte-identical to on 2-D); the 1-D/3-D/decode behaviour is pinned by libzfp-generated fixtures.
+ * Callers: tests/, __graft_entry__.smoke(), bench.py cpu_baseline.
+ */
+#include "zfp_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EBITS 8
+#define EBIAS 127
+#define NBMASK 0xaaaaaaaau
+#define OMIN(a, b) ((a) < (b) ? (a) : (b))
+#define OMAX(a, b) ((a) > (b) ? (a) : (b))
+
+/* ------------------------------------------------------------------------------------------------
+ * Bit I/O: LSB-first into little-endian uint64 words (sw/src/stream.c:61-138). Output words must
+ * be zero-initialised; bits are OR-ed in at absolute bit offsets.
+ * ---------------------------------------------------------------------------------------------- */
+static inline void put_bits(uint64_t* w, uint64_t* pos, uint64_t v, unsigned n)
+{
+  if (!n) return;
+  if (n < 64) v &= ((uint64_t)1 << n) - 1;
+  uint64_t p = *pos;
+  unsigned sh = (unsigned)(p & 63);
+  w[p >> 6] |= v << sh;
+  if (sh && sh + n > 64) w[(p >> 6) + 1] |= v >> (64 - sh);
+  *pos = p + n;
+}
+
+static inline unsigned put_bit(uint64_t* w, uint64_t* pos, unsigned bit)
+{
+  if (bit) w[*pos >> 6] |= (uint64_t)1 << (*pos & 63);
+  (*pos)++;
+  return bit;
+}
+
+static inline uint64_t get_bits(const uint64_t* w, uint64_t* pos, unsigned n)
+{
+  if (!n) return 0;
+  uint64_t p = *pos;
+  unsigned sh = (unsigned)(p & 63);
+  uint64_t v = w[p >> 6] >> sh;
+  if (sh && sh + n > 64) v |= w[(p >> 6) + 1] << (64 - sh);
+  if (n < 64) v &= ((uint64_t)1 << n) - 1;
+  *pos = p + n;
+  return v;
+}
+
+static inline unsigned get_bit(const uint64_t* w, uint64_t* pos)
+{
+  unsigned b = (unsigned)(w[*pos >> 6] >> (*pos & 63)) & 1u;
+  (*pos)++;
+  return b;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Parameters (sw/src/common.c:6-21, 226-236)
+ * ---------------------------------------------------------------------------------------------- */
+unsigned orc_precision(int emax, unsigned maxprec, int minexp, unsigned dims)
+{
+  /* common.c:226-229 */
+  int p = emax - minexp + 2 * (int)dims + 2;
+  return OMIN(maxprec, (unsigned)OMAX(0, p));
+}
+
+static int exceeded_maxbits(unsigned maxbits, unsigned maxprec, unsigned size)
+{
+  /* common.c:232-236 */
+  return (maxprec + 1) * size - 1 > maxbits;
+}
+
+void orc_set_accuracy(orc_params* p, double tol)
+{
+  /* common.c:6-21 */
+  int emin = -1074;
+  if (tol > 0) {
+    frexp(tol, &emin);
+    emin--;
+  }
+  p->minbits = 1;
+  p->maxbits = 16658; /* sw/include/common.h:11 (libzfp 16657; identical for d <= 3) */
+  p->maxprec = 64;
+  p->minexp = emin;
+}
+
+void orc_set_rate(orc_params* p, double rate, unsigned dims)
+{
+  /* libzfp 0.5.5 zfp_stream_set_rate (non-wra), float: bits = max(floor(4^d rate + 0.5), 1 + 8) */
+  unsigned n = 1u << (2 * dims);
+  unsigned bits = (unsigned)floor(n * rate + 0.5);
+  if (bits < 9) bits = 9;
+  p->minbits = bits;
+  p->maxbits = bits;
+  p->maxprec = 64;
+  p->minexp = -1074;
+}
+
+void orc_set_precision(orc_params* p, unsigned prec)
+{
+  /* libzfp 0.5.5 zfp_stream_set_precision */
+  p->minbits = 1;
+  p->maxbits = 16658;
+  p->maxprec = prec ? OMIN(prec, 64u) : 64u;
+  p->minexp = -1074;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Stages (sw/src/encode.c)
+ * ---------------------------------------------------------------------------------------------- */
+int orc_block_exponent(const float* block, unsigned n)
+{
+  /* encode.c:142-152 + get_scaler_exponent :128-140. NaN never wins `max < f`; glibc frexp(inf) -> 0. */
+  float max = 0;
+  do {
+    float f = fabsf(*block++);
+    if (max < f) max = f;
+  } while (--n);
+  int e = -EBIAS;
+  if (max > 0) {
+    frexp((double)max, &e);
+    e = OMAX(e, 1 - EBIAS);
+  }
+  return e;
+}
+
+void orc_fwd_cast(int32_t* iblock, const float* fblock, unsigned n, int emax)
+{
+  /* encode.c:162-187. scale = 2^(30-emax) (+inf when emax <= -98). x86 (int32) of NaN / out-of-range gives
+   * INT_MIN (cvttss2si "integer indefinite"); stated explicitly here so the oracle has no UB. */
+  float scale = (float)ldexp(1.0, 30 - emax);
+  do {
+    float p = scale * *fblock++;
+    *iblock++ = (fabsf(p) < 2147483648.0f) ? (int32_t)p : INT32_MIN;
+  } while (--n);
+}
+
+static inline int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+static inline int32_t wsub(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+static inline int32_t wshl1(int32_t a) { return (int32_t)((uint32_t)a << 1); }
+
+static void fwd_lift(int32_t* p, ptrdiff_t s)
+{
+  /* encode.c:189-249 with int32 wraparound made explicit */
+  int32_t x = p[0], y = p[s], z = p[2 * s], w = p[3 * s];
+  x = wadd(x, w); x >>= 1; w = wsub(w, x);
+  z = wadd(z, y); z >>= 1; y = wsub(y, z);
+  x = wadd(x, z); x >>= 1; z = wsub(z, x);
+  w = wadd(w, y); w >>= 1; y = wsub(y, w);
+  w = wadd(w, y >> 1); y = wsub(y, w >> 1);
+  p[0] = x; p[s] = y; p[2 * s] = z; p[3 * s] = w;
+}
+
+static void inv_lift(int32_t* p, ptrdiff_t s)
+{
+  /* decode.c:58-100 */
+  int32_t x = p[0], y = p[s], z = p[2 * s], w = p[3 * s];
+  y = wadd(y, w >> 1); w = wsub(w, y >> 1);
+  y = wadd(y, w); w = wshl1(w); w = wsub(w, y);
+  z = wadd(z, x); x = wshl1(x); x = wsub(x, z);
+  y = wadd(y, z); z = wshl1(z); z = wsub(z, y);
+  w = wadd(w, x); x = wshl1(x); x = wsub(x, w);
+  p[0] = x; p[s] = y; p[2 * s] = z; p[3 * s] = w;
+}
+
+void orc_fwd_xform(int32_t* q, unsigned dims)
+{
+  /* encode.c:251-260 (2-D: x then y); 1-D one lift; 3-D x, y, z as libzfp */
+  unsigned x, y, z;
+  switch (dims) {
+    case 1:
+      fwd_lift(q, 1);
+      break;
+    case 2:
+      for (y = 0; y < 4; y++) fwd_lift(q + 4 * y, 1);
+      for (x = 0; x < 4; x++) fwd_lift(q + x, 4);
+      break;
+    case 3:
+      for (z = 0; z < 4; z++)
+        for (y = 0; y < 4; y++) fwd_lift(q + 4 * y + 16 * z, 1);
+      for (x = 0; x < 4; x++)
+        for (z = 0; z < 4; z++) fwd_lift(q + 16 * z + x, 4);
+      for (y = 0; y < 4; y++)
+        for (x = 0; x < 4; x++) fwd_lift(q + x + 4 * y, 16);
+      break;
+  }
+}
+
+void orc_inv_xform(int32_t* q, unsigned dims)
+{
+  /* decode.c:102-111 (2-D: y then x); 3-D z, y, x */
+  unsigned x, y, z;
+  switch (dims) {
+    case 1:
+      inv_lift(q, 1);
+      break;
+    case 2:
+      for (x = 0; x < 4; x++) inv_lift(q + x, 4);
+      for (y = 0; y < 4; y++) inv_lift(q + 4 * y, 1);
+      break;
+    case 3:
+      for (y = 0; y < 4; y++)
+        for (x = 0; x < 4; x++) inv_lift(q + x + 4 * y, 16);
+      for (x = 0; x < 4; x++)
+        for (z = 0; z < 4; z++) inv_lift(q + 16 * z + x, 4);
+      for (z = 0; z < 4; z++)
+        for (y = 0; y < 4; y++) inv_lift(q + 4 * y + 16 * z, 1);
+      break;
+  }
+}
+
+static const unsigned char PERM1[4] = {0, 1, 2, 3};
+/* sw/include/types.h:71-97 */
+static const unsigned char PERM2[16] = {0, 1, 4, 5, 2, 8, 6, 9, 3, 12, 10, 7, 13, 11, 14, 15};
+/* libzfp 0.5.5 perm_3 (ordered by i+j+k, then i^2+j^2+k^2); SURVEY 8(a) A11 */
+static const unsigned char PERM3[64] = {
+    0,  1,  4,  16, 20, 17, 5,  2,  8,  32, 21, 6,  18, 24, 9,  33, 36, 3,  12, 48, 22, 25,
+    37, 40, 34, 10, 7,  19, 28, 13, 49, 52, 41, 38, 26, 23, 29, 53, 11, 35, 44, 14, 50, 56,
+    42, 27, 39, 45, 30, 54, 57, 60, 51, 15, 43, 46, 58, 61, 55, 31, 62, 59, 47, 63};
+
+const unsigned char* orc_perm(unsigned dims)
+{
+  return dims == 1 ? PERM1 : dims == 2 ? PERM2 : PERM3;
+}
+
+void orc_fwd_reorder(uint32_t* u, const int32_t* q, unsigned dims)
+{
+  /* encode.c:263-275 (without the one-past-the-end write of :272-274) */
+  const unsigned char* perm = orc_perm(dims);
+  unsigned size = 1u << (2 * dims);
+  for (unsigned i = 0; i < size; i++) u[i] = ((uint32_t)q[perm[i]] + NBMASK) ^ NBMASK;
+}
+
+unsigned orc_encode_ints(uint64_t* w, uint64_t* pos, const uint32_t* u, unsigned maxbits, unsigned maxprec,
+                         unsigned size)
+{
+  /* encode.c:279-339 (partial) == encode.c:343-408 (all) whenever the budget is not hit */
+  unsigned intprec = 32;
+  unsigned kmin = intprec > maxprec ? intprec - maxprec : 0;
+  unsigned bits = maxbits;
+  unsigned i, k, m, n;
+  for (k = intprec, n = 0; bits && k-- > kmin;) {
+    uint64_t x = 0;
+    for (i = 0; i < size; i++) x += (uint64_t)((u[i] >> k) & 1u) << i;
+    m = OMIN(n, bits);
+    bits -= m;
+    put_bits(w, pos, x, m);
+    x = m < 64 ? x >> m : 0;
+    for (; bits && n < size; x >>= 1, n++) {
+      bits--;
+      if (put_bit(w, pos, !!x)) {
+        for (; bits && n < size - 1; x >>= 1, n++) {
+          bits--;
+          if (put_bit(w, pos, (unsigned)(x & 1u))) break;
+        }
+      } else {
+        break;
+      }
+    }
+  }
+  return maxbits - bits;
+}
+
+unsigned orc_encode_iblock(uint64_t* w, uint64_t* pos, unsigned minbits, unsigned maxbits, unsigned maxprec,
+                           int32_t* q, unsigned dims)
+{
+  /* encode.c:412-455 */
+  unsigned size = 1u << (2 * dims);
+  uint32_t u[64];
+  orc_fwd_xform(q, dims);
+  orc_fwd_reorder(u, q, dims);
+  unsigned budget = exceeded_maxbits(maxbits, maxprec, size) ? maxbits : ~0u;
+  unsigned bits = orc_encode_ints(w, pos, u, budget, maxprec, size);
+  if (bits < minbits) {
+    *pos += minbits - bits; /* stream_pad: zero bits */
+    bits = minbits;
+  }
+  return bits;
+}
+
+unsigned orc_encode_fblock(uint64_t* w, uint64_t* pos, const orc_params* p, const float* f, unsigned dims)
+{
+  /* encode.c:457-495 */
+  unsigned bits = 1;
+  unsigned size = 1u << (2 * dims);
+  int emax = orc_block_exponent(f, size);
+  unsigned maxprec = orc_precision(emax, p->maxprec, p->minexp, dims);
+  unsigned e = maxprec ? (unsigned)(emax + EBIAS) : 0;
+  if (e) {
+    int32_t q[64];
+    bits += EBITS;
+    put_bits(w, pos, 2 * (uint64_t)e + 1, bits);
+    orc_fwd_cast(q, f, size, emax);
+    bits += orc_encode_iblock(w, pos, p->minbits - OMIN(bits, p->minbits), p->maxbits - bits, maxprec, q, dims);
+  } else {
+    put_bit(w, pos, 0);
+    if (p->minbits > bits) {
+      *pos += p->minbits - bits;
+      bits = p->minbits;
+    }
+  }
+  return bits;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Gather / scatter with partial-block padding (encode.c:41-126, decode.c:27-42)
+ * ---------------------------------------------------------------------------------------------- */
+static inline size_t pad_index(size_t i, size_t nvalid)
+{
+  /* pad_partial_block fall-through (encode.c:41-60): n=1 -> v0 v0 v0 v0; n=2 -> v0 v1 v1 v0; n=3 -> v0 v1 v2 v0 */
+  switch (nvalid) {
+    case 1: return 0;
+    case 2: return i == 3 ? 0 : (i == 2 ? 1 : i);
+    case 3: return i == 3 ? 0 : i;
+    default: return i;
+  }
+}
+
+static inline float load_value(const void* data, int dtype, ptrdiff_t off)
+{
+  if (dtype == ORC_BF16) {
+    uint32_t b = (uint32_t)((const uint16_t*)data)[off] << 16;
+    float f;
+    memcpy(&f, &b, 4);
+    return f;
+  }
+  return ((const float*)data)[off];
+}
+
+static void default_strides(unsigned dims, const size_t* n, const ptrdiff_t* s, ptrdiff_t* out)
+{
+  out[0] = s && s[0] ? s[0] : 1;
+  out[1] = s && dims > 1 && s[1] ? s[1] : (ptrdiff_t)n[0];
+  out[2] = s && dims > 2 && s[2] ? s[2] : (ptrdiff_t)(n[0] * (dims > 1 ? n[1] : 1));
+}
+
+void orc_gather_block(float* block, const void* data, int dtype, unsigned dims, const size_t* n,
+                      const ptrdiff_t* s, const size_t* b)
+{
+  ptrdiff_t st[3];
+  default_strides(dims, n, s, st);
+  size_t nv[3] = {1, 1, 1};
+  for (unsigned a = 0; a < dims; a++) nv[a] = OMIN((size_t)4, n[a] - 4 * b[a]);
+  unsigned ez = dims > 2 ? 4 : 1, ey = dims > 1 ? 4 : 1;
+  for (unsigned z = 0; z < ez; z++)
+    for (unsigned y = 0; y < ey; y++)
+      for (unsigned x = 0; x < 4; x++) {
+        ptrdiff_t off = (ptrdiff_t)(4 * b[0] + pad_index(x, nv[0])) * st[0];
+        if (dims > 1) off += (ptrdiff_t)(4 * b[1] + pad_index(y, nv[1])) * st[1];
+        if (dims > 2) off += (ptrdiff_t)(4 * b[2] + pad_index(z, nv[2])) * st[2];
+        block[16 * z + 4 * y + x] = load_value(data, dtype, off);
+      }
+}
+
+static void scatter_block(const float* block, float* data, unsigned dims, const size_t* n, const ptrdiff_t* st,
+                          const size_t* b)
+{
+  size_t nv[3] = {1, 1, 1};
+  for (unsigned a = 0; a < dims; a++) nv[a] = OMIN((size_t)4, n[a] - 4 * b[a]);
+  for (unsigned z = 0; z < nv[2]; z++)
+    for (unsigned y = 0; y < nv[1]; y++)
+      for (unsigned x = 0; x < nv[0]; x++) {
+        ptrdiff_t off = (ptrdiff_t)(4 * b[0] + x) * st[0];
+        if (dims > 1) off += (ptrdiff_t)(4 * b[1] + y) * st[1];
+        if (dims > 2) off += (ptrdiff_t)(4 * b[2] + z) * st[2];
+        data[off] = block[16 * z + 4 * y + x];
+      }
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Array driver (zfp.c:10-56): traversal z, y, x; flush to 64 bits.
+ * ---------------------------------------------------------------------------------------------- */
+size_t orc_num_blocks(unsigned dims, const size_t* n)
+{
+  size_t nb = 1;
+  for (unsigned a = 0; a < dims; a++) nb *= (n[a] + 3) / 4;
+  return nb;
+}
+
+static inline void block_coords(size_t idx, unsigned dims, const size_t* n, size_t* b)
+{
+  size_t bx = (n[0] + 3) / 4;
+  size_t by = dims > 1 ? (n[1] + 3) / 4 : 1;
+  b[0] = idx % bx;
+  b[1] = (idx / bx) % by;
+  b[2] = idx / (bx * by);
+}
+
+static uint64_t compress_range(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
+                               const orc_params* p, size_t first, size_t last, uint64_t* out)
+{
+  uint64_t pos = 0;
+  float f[64];
+  size_t b[3];
+  for (size_t i = first; i < last; i++) {
+    block_coords(i, dims, n, b);
+    orc_gather_block(f, data, dtype, dims, n, s, b);
+    orc_encode_fblock(out, &pos, p, f, dims);
+  }
+  return pos;
+}
+
+static size_t max_block_bits(const orc_params* p, unsigned dims)
+{
+  unsigned size = 1u << (2 * dims);
+  size_t mb = 9 + (size - 1) + (size_t)size * OMIN(p->maxprec, 32u); /* common.c:187-224 */
+  if (p->maxbits >= 9) mb = OMIN(mb, (size_t)p->maxbits);
+  return OMAX(mb, (size_t)p->minbits);
+}
+
+uint64_t orc_compress(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
+                      const orc_params* p, uint64_t* out, size_t out_words)
+{
+  memset(out, 0, out_words * 8);
+  return compress_range(data, dtype, dims, n, s, p, 0, orc_num_blocks(dims, n), out);
+}
+
+typedef struct {
+  const void* data;
+  int dtype;
+  unsigned dims;
+  const size_t* n;
+  const ptrdiff_t* s;
+  const orc_params* p;
+  size_t first, last;
+  uint64_t* buf;
+  uint64_t bits;
+} shard_job;
+
+static void* shard_main(void* arg)
+{
+  shard_job* j = (shard_job*)arg;
+  j->bits = compress_range(j->data, j->dtype, j->dims, j->n, j->s, j->p, j->first, j->last, j->buf);
+  return NULL;
+}
+
+static void stitch(uint64_t* out, uint64_t off, const uint64_t* src, uint64_t bits)
+{
+  /* Append `bits` bits of src at bit offset `off` (out zeroed). */
+  uint64_t nw = (bits + 63) / 64;
+  unsigned sh = (unsigned)(off & 63);
+  uint64_t base = off >> 6;
+  for (uint64_t i = 0; i < nw; i++) {
+    uint64_t v = src[i];
+    if (i == nw - 1 && (bits & 63)) v &= ((uint64_t)1 << (bits & 63)) - 1;
+    out[base + i] |= v << sh;
+    if (sh) {
+      uint64_t hi = v >> (64 - sh);
+      if (hi) out[base + i + 1] |= hi;
+    }
+  }
+}
+
+uint64_t orc_compress_mt(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
+                         const orc_params* p, uint64_t* out, size_t out_words, int nthreads)
+{
+  size_t nb = orc_num_blocks(dims, n);
+  if (nthreads < 1) nthreads = 1;
+  if ((size_t)nthreads > nb) nthreads = (int)(nb ? nb : 1);
+  shard_job* jobs = (shard_job*)calloc((size_t)nthreads, sizeof(shard_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  size_t per = (nb + nthreads - 1) / nthreads;
+  size_t mbb = max_block_bits(p, dims);
+  for (int t = 0; t < nthreads; t++) {
+    shard_job* j = &jobs[t];
+    j->data = data; j->dtype = dtype; j->dims = dims; j->n = n; j->s = s; j->p = p;
+    j->first = OMIN(nb, (size_t)t * per);
+    j->last = OMIN(nb, j->first + per);
+    size_t words = ((j->last - j->first) * mbb + 63) / 64 + 2;
+    j->buf = (uint64_t*)calloc(words, 8);
+    pthread_create(&th[t], NULL, shard_main, j);
+  }
+  memset(out, 0, out_words * 8);
+  uint64_t off = 0;
+  for (int t = 0; t < nthreads; t++) {
+    pthread_join(th[t], NULL);
+    stitch(out, off, jobs[t].buf, jobs[t].bits);
+    off += jobs[t].bits;
+    free(jobs[t].buf);
+  }
+  free(jobs);
+  free(th);
+  return off;
+}
+
+void orc_block_bits(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
+                    const orc_params* p, uint32_t* bits_out)
+{
+  size_t nb = orc_num_blocks(dims, n);
+  uint64_t scratch[300];
+  float f[64];
+  size_t b[3];
+  for (size_t i = 0; i < nb; i++) {
+    uint64_t pos = 0;
+    memset(scratch, 0, sizeof(scratch));
+    block_coords(i, dims, n, b);
+    orc_gather_block(f, data, dtype, dims, n, s, b);
+    bits_out[i] = orc_encode_fblock(scratch, &pos, p, f, dims);
+  }
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Decoder (libzfp 0.5.5 semantics; sw/src/decode.c:113-253 with block size 4^d)
+ * ---------------------------------------------------------------------------------------------- */
+static unsigned decode_ints(const uint64_t* w, uint64_t* pos, unsigned maxbits, unsigned maxprec, uint32_t* u,
+                            unsigned size)
+{
+  /* decode.c:141-183 */
+  unsigned intprec = 32;
+  unsigned kmin = intprec > maxprec ? intprec - maxprec : 0;
+  unsigned bits = maxbits;
+  unsigned i, k, m, n;
+  for (i = 0; i < size; i++) u[i] = 0;
+  for (k = intprec, n = 0; bits && k-- > kmin;) {
+    m = OMIN(n, bits);
+    bits -= m;
+    uint64_t x = get_bits(w, pos, m);
+    for (; n < size && bits && (bits--, get_bit(w, pos)); x += (uint64_t)1 << n++)
+      for (; n < size - 1 && bits && (bits--, !get_bit(w, pos)); n++)
+        ;
+    for (i = 0; x; i++, x >>= 1) u[i] += (uint32_t)(x & 1u) << k;
+  }
+  return maxbits - bits;
+}
+
+static unsigned decode_fblock(const uint64_t* w, uint64_t* pos, const orc_params* p, float* f, unsigned dims)
+{
+  /* decode.c:220-253 + decode_iblock :185-218 */
+  unsigned size = 1u << (2 * dims);
+  unsigned bits = 1;
+  if (get_bit(w, pos)) {
+    bits += EBITS;
+    int emax = (int)get_bits(w, pos, EBITS) - EBIAS;
+    unsigned maxprec = orc_precision(emax, p->maxprec, p->minexp, dims);
+    unsigned minb = p->minbits - OMIN(bits, p->minbits);
+    unsigned maxb = p->maxbits - bits;
+    uint32_t u[64];
+    int32_t q[64];
+    unsigned budget = exceeded_maxbits(maxb, maxprec, size) ? maxb : ~0u;
+    unsigned got = decode_ints(w, pos, budget, maxprec, u, size);
+    if (got < minb) {
+      *pos += minb - got;
+      got = minb;
+    }
+    bits += got;
+    const unsigned char* perm = orc_perm(dims);
+    for (unsigned i = 0; i < size; i++) q[perm[i]] = (int32_t)((u[i] ^ NBMASK) - NBMASK); /* decode.c:44-56 */
+    orc_inv_xform(q, dims);
+    float sc = ldexpf(1.0f, emax - 30); /* decode.c:12-25 dequantize */
+    for (unsigned i = 0; i < size; i++) f[i] = (float)(sc * (float)q[i]);
+  } else {
+    for (unsigned i = 0; i < size; i++) f[i] = 0;
+    if (p->minbits > bits) {
+      *pos += p->minbits - bits;
+      bits = p->minbits;
+    }
+  }
+  return bits;
+}
+
+uint64_t orc_decompress(float* data, unsigned dims, const size_t* n, const ptrdiff_t* s, const orc_params* p,
+                        const uint64_t* in, size_t in_words)
+{
+  (void)in_words;
+  ptrdiff_t st[3];
+  default_strides(dims, n, s, st);
+  size_t nb = orc_num_blocks(dims, n);
+  uint64_t pos = 0;
+  float f[64];
+  size_t b[3];
+  for (size_t i = 0; i < nb; i++) {
+    block_coords(i, dims, n, b);
+    decode_fblock(in, &pos, p, f, dims);
+    scatter_block(f, data, dims, n, st, b);
+  }
+  return pos;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Deterministic inputs
+ * ---------------------------------------------------------------------------------------------- */
+void orc_gen_bump2d(float* out, size_t n, int f32sum)
+{
+  /* sw/tests/test_zfp.cpp:13-25; f32sum: x*x + y*y summed in float32 (recipe that reproduces the
+   * 530/550/590/600 goldens) */
+  for (size_t j = 0; j < n; j++)
+    for (size_t i = 0; i < n; i++) {
+      double x = 2.0 * i / n;
+      double y = 2.0 * j / n;
+      if (f32sum) {
+        float xf = (float)x, yf = (float)y;
+        float r = xf * xf + yf * yf;
+        out[i + n * j] = (float)exp(-(double)r);
+      } else {
+        out[i + n * j] = (float)exp(-(x * x + y * y));
+      }
+    }
+}
+
+static inline uint64_t splitmix64(uint64_t* st)
+{
+  uint64_t z = (*st += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+void orc_gen_normal(float* out, size_t count, double sigma, uint64_t seed, int inject)
+{
+  /* splitmix64, Box-Muller in double then cast; injected zero / tiny (INT_MIN path) / subnormal
+   * 4-value blocks at rates 1/64, 1/4096, 1/4096. */
+  uint64_t st = seed;
+  for (size_t i = 0; i < count; i += 2) {
+    double u1 = ((double)(splitmix64(&st) >> 11) + 1.0) * 0x1.0p-53;
+    double u2 = (double)(splitmix64(&st) >> 11) * 0x1.0p-53;
+    double r = sqrt(-2.0 * log(u1));
+    out[i] = (float)(sigma * r * cos(6.283185307179586 * u2));
+    if (i + 1 < count) out[i + 1] = (float)(sigma * r * sin(6.283185307179586 * u2));
+  }
+  if (!inject) return;
+  for (size_t blk = 0; blk * 4 < count; blk++) {
+    uint64_t h = blk ^ seed;
+    h = splitmix64(&h);
+    double scale;
+    if (h % 64 == 0) scale = 0.0;
+    else if (h % 4096 == 1) scale = 1e-35 / sigma;
+    else if (h % 4096 == 2) scale = 1e-40 / sigma;
+    else continue;
+    for (size_t k = 4 * blk; k < count && k < 4 * blk + 4; k++) out[k] = (float)((double)out[k] * scale);
+  }
+}
