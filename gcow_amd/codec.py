@@ -1,0 +1,218 @@
+"""Host-side API over libgcow.so for device-resident torch tensors.
+
+Mirrors the reference's codec interface (fpgasystems/gcow sw/include/types.h + zfp.h): the four expert parameters
+(minbits, maxbits, maxprec, minexp) and the accuracy / rate / precision setters, `encode` = zfp_compress
+(sw/src/zfp.c:10-28) and `decode` = zfp_decompress with libzfp 0.5.5 semantics. torch is used only for device
+memory and streams; every byte of codec work runs in the gfx950 kernels of gcow_amd/csrc.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+
+import torch
+
+from ._ffi import DTYPE_BF16, DTYPE_FLOAT, GcowError, GcowParams, ZfpInput, check, load
+
+ZFP_MIN_BITS, ZFP_MAX_BITS, ZFP_MAX_PREC, ZFP_MIN_EXP = 1, 16658, 64, -1074
+
+
+# ------------------------------------------------------------------------------------------- parameters
+def accuracy(tolerance: float) -> GcowParams:
+    """set_zfp_output_accuracy (sw/src/common.c:6-21)."""
+    emin = ZFP_MIN_EXP
+    if tolerance > 0:
+        _, e = math.frexp(tolerance)
+        emin = e - 1
+    return GcowParams(ZFP_MIN_BITS, ZFP_MAX_BITS, ZFP_MAX_PREC, emin)
+
+
+def rate(bits_per_value: float, dims: int) -> GcowParams:
+    """libzfp 0.5.5 zfp_stream_set_rate (float, no write-random-access): minbits = maxbits = floor(4^d r + 0.5)."""
+    n = 1 << (2 * dims)
+    bits = max(int(math.floor(n * bits_per_value + 0.5)), 9)
+    return GcowParams(bits, bits, ZFP_MAX_PREC, ZFP_MIN_EXP)
+
+
+def precision(prec: int) -> GcowParams:
+    """libzfp 0.5.5 zfp_stream_set_precision."""
+    p = min(prec, ZFP_MAX_PREC) if prec else ZFP_MAX_PREC
+    return GcowParams(ZFP_MIN_BITS, ZFP_MAX_BITS, p, ZFP_MIN_EXP)
+
+
+def expert(minbits: int, maxbits: int, maxprec: int, minexp: int) -> GcowParams:
+    return GcowParams(minbits, maxbits, maxprec, minexp)
+
+
+def is_fixed(p: GcowParams) -> bool:
+    return p.minbits == p.maxbits
+
+
+# ------------------------------------------------------------------------------------------- fields
+def field_of(t: torch.Tensor, dims: int | None = None) -> ZfpInput:
+    """zfp_input for a 1-3 dim tensor (numpy order: the last axis is x, the fastest)."""
+    if t.dim() < 1 or t.dim() > 3:
+        raise GcowError("tensors of 1-3 dims are supported, got %d" % t.dim())
+    if t.dtype == torch.float32:
+        dt = DTYPE_FLOAT
+    elif t.dtype == torch.bfloat16:
+        dt = DTYPE_BF16
+    else:
+        raise GcowError("dtype %s not supported (float32, bfloat16)" % t.dtype)
+    f = ZfpInput()
+    f.dtype = dt
+    f.data = t.data_ptr()
+    shp = list(reversed(t.shape))
+    st = list(reversed(t.stride()))
+    names_n = ["nx", "ny", "nz"]
+    names_s = ["sx", "sy", "sz"]
+    for i in range(t.dim()):
+        setattr(f, names_n[i], int(shp[i]))
+        setattr(f, names_s[i], int(st[i]))
+    return f
+
+
+def _stream_ptr(stream) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def max_output_bytes(shape, p: GcowParams, dtype=torch.float32) -> int:
+    t = torch.empty(0)
+    f = ZfpInput()
+    f.dtype = DTYPE_FLOAT if dtype == torch.float32 else DTYPE_BF16
+    shp = list(reversed(shape))
+    for i, n in enumerate(shp):
+        setattr(f, ["nx", "ny", "nz"][i], int(n))
+    del t
+    return load().gcow_max_output_bytes(C.byref(f), C.byref(p))
+
+
+@dataclass
+class Encoded:
+    """A compressed stream on the device: `words` (int64 tensor holding little-endian uint64 stream words),
+    `bits_dev` (int64[1] device tensor with the unflushed bit count), optional block `index` for parallel decode."""
+    words: torch.Tensor
+    bits_dev: torch.Tensor
+    shape: tuple
+    params: GcowParams
+    index: torch.Tensor | None = None
+    index_stride: int = 0
+
+    @property
+    def bits(self) -> int:
+        return int(self.bits_dev.item())
+
+    @property
+    def nwords(self) -> int:
+        return (self.bits + 63) // 64
+
+    def stream(self) -> torch.Tensor:
+        """The flushed stream: ceil(bits/64) words (sw/src/stream.c:132-138 + :176-179)."""
+        return self.words[: self.nwords]
+
+    def to_bytes(self) -> bytes:
+        return self.stream().cpu().numpy().tobytes()
+
+
+class Encoder:
+    """Preallocated encoder for a fixed shape / dtype / params (bench and repeated-bucket use)."""
+
+    def __init__(self, shape, dtype, params: GcowParams, device=None, index_stride: int = 0):
+        self.L = load()
+        self.shape = tuple(shape)
+        self.dtype = dtype
+        self.params = params
+        self.device = torch.device(device or "cuda")
+        f = field_of_shape(self.shape, dtype)
+        self.cap = self.L.gcow_max_output_bytes(C.byref(f), C.byref(params))
+        if self.cap == 0:
+            raise GcowError("unsupported shape %s" % (self.shape,))
+        self.words = torch.zeros((self.cap + 7) // 8, dtype=torch.int64, device=self.device)
+        self.bits_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.fixed = is_fixed(params)
+        if self.fixed:  # fixed rate: the bit count is known on the host; no device write per call
+            nb = 1
+            for n in self.shape:
+                nb *= (n + 3) // 4
+            self.bits_dev.fill_(nb * params.maxbits)
+        ws = self.L.gcow_encode_workspace_bytes(C.byref(f), C.byref(params))
+        self.ws = torch.zeros(max(ws // 8, 1), dtype=torch.int64, device=self.device)
+        self.ws_bytes = ws
+        self.index_stride = index_stride
+        ne = self.L.gcow_index_entries(C.byref(f), index_stride) if index_stride else 0
+        self.index = torch.zeros(max(ne, 1), dtype=torch.int64, device=self.device) if index_stride else None
+
+    def __call__(self, x: torch.Tensor, stream=None) -> Encoded:
+        if tuple(x.shape) != self.shape or x.dtype != self.dtype:
+            raise GcowError("Encoder built for %s %s, got %s %s" % (self.shape, self.dtype, tuple(x.shape), x.dtype))
+        if not x.is_cuda:
+            raise GcowError("Encoder expects a device tensor")
+        f = field_of(x)
+        st = self.L.gcow_encode_device(C.byref(f), C.byref(self.params), self.words.data_ptr(), self.cap,
+                                       None if self.fixed else self.bits_dev.data_ptr(), self.ws.data_ptr(),
+                                       self.ws_bytes,
+                                       self.index.data_ptr() if self.index is not None else None,
+                                       self.index_stride, _stream_ptr(stream))
+        check(st, "gcow_encode_device")
+        return Encoded(self.words, self.bits_dev, self.shape, self.params, self.index, self.index_stride)
+
+
+def field_of_shape(shape, dtype) -> ZfpInput:
+    f = ZfpInput()
+    f.dtype = DTYPE_BF16 if dtype == torch.bfloat16 else DTYPE_FLOAT
+    for i, n in enumerate(reversed(tuple(shape))):
+        setattr(f, ["nx", "ny", "nz"][i], int(n))
+    return f
+
+
+def encode(x: torch.Tensor, params: GcowParams, index_stride: int = 0, stream=None) -> Encoded:
+    """zfp_compress of a device tensor (1-3 dims, fp32 or bf16, any strides)."""
+    if not x.is_cuda:
+        raise GcowError("encode expects a device tensor (use gcow_amd.dropin for host arrays)")
+    enc = Encoder(x.shape, x.dtype, params, x.device, index_stride)
+    L = enc.L
+    f = field_of(x)
+    st = L.gcow_encode_device(C.byref(f), C.byref(params), enc.words.data_ptr(), enc.cap, enc.bits_dev.data_ptr(),
+                              enc.ws.data_ptr(), enc.ws_bytes,
+                              enc.index.data_ptr() if enc.index is not None else None, index_stride,
+                              _stream_ptr(stream))
+    check(st, "gcow_encode_device")
+    return Encoded(enc.words, enc.bits_dev, tuple(x.shape), params, enc.index, index_stride)
+
+
+def decode(enc_or_words, shape=None, params: GcowParams | None = None, index: torch.Tensor | None = None,
+           index_stride: int = 0, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """zfp_decompress (libzfp 0.5.5 semantics) into an fp32 device tensor."""
+    if isinstance(enc_or_words, Encoded):
+        e = enc_or_words
+        words, shape, params = e.words, e.shape, e.params
+        if index is None and e.index is not None:
+            index, index_stride = e.index, e.index_stride
+    else:
+        words = enc_or_words
+    if out is None:
+        out = torch.empty(tuple(shape), dtype=torch.float32, device=words.device)
+    f = field_of(out)
+    L = load()
+    st = L.gcow_decode_device(C.byref(f), C.byref(params), words.data_ptr(), words.numel() * 8,
+                              index.data_ptr() if index is not None else None, index_stride, _stream_ptr(stream))
+    check(st, "gcow_decode_device")
+    return out
+
+
+def stitch(dst: torch.Tensor, dst_bit_offset: int, src: torch.Tensor, src_bits: int, stream=None):
+    """OR src_bits bits of src into dst at dst_bit_offset (device words; dst zeroed beyond earlier content)."""
+    L = load()
+    check(L.gcow_stitch_device(dst.data_ptr(), dst_bit_offset, src.data_ptr(), src_bits, _stream_ptr(stream)),
+          "gcow_stitch_device")
+
+
+def fill_normal(out: torch.Tensor, sigma: float = 1e-3, seed: int = 0x67636F77, inject: bool = True, stream=None):
+    """Deterministic synthetic gradient bucket on the device (SURVEY 8(d) distribution)."""
+    assert out.dtype == torch.float32 and out.is_cuda and out.is_contiguous()
+    check(load().gcow_fill_normal_device(out.data_ptr(), out.numel(), sigma, seed, int(inject),
+                                         _stream_ptr(stream)), "gcow_fill_normal_device")
+    return out

@@ -1,0 +1,424 @@
+// codec_device.h -- per-block ZFP-style codec primitives for CDNA4 (gfx950), one block per lane.
+//
+// Every function restates one stage of gcow's sw/ encoder (fpgasystems/gcow sw/src/encode.c) or libzfp 0.5.5's
+// decoder (the semantics sw/src/decode.c intends), cited per function. Bit-exactness notes:
+//   * block exponent is computed on the IEEE bit patterns (max over non-NaN |x|; Inf -> 0 as glibc frexp);
+//   * the float->int cast emulates x86 cvttss2si: NaN / +-Inf / out-of-range -> INT_MIN (AMD's v_cvt_i32_f32
+//     saturates instead, so the range test is explicit);
+//   * lifting uses uint32 add/sub (int32 wraparound) and arithmetic right shifts;
+//   * the embedded coder emits the untruncated code and the writer drops bits beyond the block budget -- the
+//     budgeted coder's output (encode.c:279-339) is exactly that prefix.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gcow {
+
+enum : uint32_t { DT_F32 = 3, DT_BF16 = 5 };
+
+struct Params {
+  uint32_t minbits, maxbits, maxprec;
+  int32_t minexp;
+};
+
+// ------------------------------------------------------------------------------------------------ constants
+template <int D> struct Dim;
+template <> struct Dim<1> { static constexpr int B = 4; };
+template <> struct Dim<2> { static constexpr int B = 16; };
+template <> struct Dim<3> { static constexpr int B = 64; };
+
+// sw/include/types.h:71-97 PERM_2D; identity for 1-D; libzfp 0.5.5 perm_3 for 3-D.
+__device__ __host__ constexpr int perm_index(int D, int i)
+{
+  constexpr uint8_t P2[16] = {0, 1, 4, 5, 2, 8, 6, 9, 3, 12, 10, 7, 13, 11, 14, 15};
+  constexpr uint8_t P3[64] = {0,  1,  4,  16, 20, 17, 5,  2,  8,  32, 21, 6,  18, 24, 9,  33,
+                              36, 3,  12, 48, 22, 25, 37, 40, 34, 10, 7,  19, 28, 13, 49, 52,
+                              41, 38, 26, 23, 29, 53, 11, 35, 44, 14, 50, 56, 42, 27, 39, 45,
+                              30, 54, 57, 60, 51, 15, 43, 46, 58, 61, 55, 31, 62, 59, 47, 63};
+  return D == 1 ? i : (D == 2 ? P2[i] : P3[i]);
+}
+
+template <int B> struct PlaneType { using T = uint32_t; };
+template <> struct PlaneType<64> { using T = uint64_t; };
+
+__device__ __forceinline__ uint64_t lowmask64(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
+
+// ------------------------------------------------------------------------------------------------ stages
+// get_block_exponent + get_scaler_exponent (encode.c:128-152) on bit patterns.
+template <int B>
+__device__ __forceinline__ int block_emax(const float (&f)[B])
+{
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < B; i++) {
+    uint32_t a = __float_as_uint(f[i]) & 0x7fffffffu;
+    m = (a <= 0x7f800000u && a > m) ? a : m;  // `max < f` never lets a NaN win
+  }
+  int e = (int)(m >> 23) - 126;
+  e = e < -126 ? -126 : e;                       // MAX(e, 1 - EBIAS): subnormals clamp to -126
+  return m == 0 ? -127 : (m >= 0x7f800000u ? 0 : e);  // zero -> -EBIAS; Inf -> 0 (glibc frexp)
+}
+
+// get_precision (sw/src/common.c:226-229)
+__device__ __forceinline__ uint32_t precision(int emax, uint32_t maxprec, int minexp, int dims)
+{
+  int p = emax - minexp + 2 * dims + 2;
+  uint32_t up = p > 0 ? (uint32_t)p : 0u;
+  return up < maxprec ? up : maxprec;
+}
+
+// quantize_scaler / fwd_cast_block (encode.c:162-187): (int32)(2^(30-emax) * x) with x86 semantics.
+__device__ __forceinline__ float cast_scale(int emax)
+{
+  int se = 30 - emax;  // >= -98, so the scale is a normal float or +inf
+  return se >= 128 ? __uint_as_float(0x7f800000u) : __uint_as_float((uint32_t)(se + 127) << 23);
+}
+
+__device__ __forceinline__ int32_t cast1(float x, float scale)
+{
+  float p = scale * x;
+  return (__builtin_fabsf(p) < 2147483648.0f) ? (int32_t)p : (int32_t)0x80000000;
+}
+
+// fwd_lift_vector (encode.c:189-249), int32 wraparound made explicit.
+__device__ __forceinline__ void fwd_lift(int32_t& x, int32_t& y, int32_t& z, int32_t& w)
+{
+  auto add = [](int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); };
+  auto sub = [](int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); };
+  x = add(x, w); x >>= 1; w = sub(w, x);
+  z = add(z, y); z >>= 1; y = sub(y, z);
+  x = add(x, z); x >>= 1; z = sub(z, x);
+  w = add(w, y); w >>= 1; y = sub(y, w);
+  w = add(w, y >> 1); y = sub(y, w >> 1);
+}
+
+// bwd_lift_vector (decode.c:58-100)
+__device__ __forceinline__ void inv_lift(int32_t& x, int32_t& y, int32_t& z, int32_t& w)
+{
+  auto add = [](int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); };
+  auto sub = [](int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); };
+  auto shl = [](int32_t a) { return (int32_t)((uint32_t)a << 1); };
+  y = add(y, w >> 1); w = sub(w, y >> 1);
+  y = add(y, w); w = shl(w); w = sub(w, y);
+  z = add(z, x); x = shl(x); x = sub(x, z);
+  y = add(y, z); z = shl(z); z = sub(z, y);
+  w = add(w, x); x = shl(x); x = sub(x, w);
+}
+
+// fwd_decorrelate (encode.c:251-260: x then y; 3-D x, y, z as libzfp)
+template <int D>
+__device__ __forceinline__ void fwd_xform(int32_t* q)
+{
+  if constexpr (D == 1) {
+    fwd_lift(q[0], q[1], q[2], q[3]);
+  } else if constexpr (D == 2) {
+#pragma unroll
+    for (int y = 0; y < 4; y++) fwd_lift(q[4 * y + 0], q[4 * y + 1], q[4 * y + 2], q[4 * y + 3]);
+#pragma unroll
+    for (int x = 0; x < 4; x++) fwd_lift(q[x + 0], q[x + 4], q[x + 8], q[x + 12]);
+  } else {
+#pragma unroll
+    for (int z = 0; z < 4; z++)
+#pragma unroll
+      for (int y = 0; y < 4; y++) {
+        int b = 16 * z + 4 * y;
+        fwd_lift(q[b + 0], q[b + 1], q[b + 2], q[b + 3]);
+      }
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+      for (int z = 0; z < 4; z++) {
+        int b = 16 * z + x;
+        fwd_lift(q[b + 0], q[b + 4], q[b + 8], q[b + 12]);
+      }
+#pragma unroll
+    for (int y = 0; y < 4; y++)
+#pragma unroll
+      for (int x = 0; x < 4; x++) {
+        int b = 4 * y + x;
+        fwd_lift(q[b + 0], q[b + 16], q[b + 32], q[b + 48]);
+      }
+  }
+}
+
+// bwd_decorrelate (decode.c:102-111: y then x; 3-D z, y, x)
+template <int D>
+__device__ __forceinline__ void inv_xform(int32_t* q)
+{
+  if constexpr (D == 1) {
+    inv_lift(q[0], q[1], q[2], q[3]);
+  } else if constexpr (D == 2) {
+#pragma unroll
+    for (int x = 0; x < 4; x++) inv_lift(q[x + 0], q[x + 4], q[x + 8], q[x + 12]);
+#pragma unroll
+    for (int y = 0; y < 4; y++) inv_lift(q[4 * y + 0], q[4 * y + 1], q[4 * y + 2], q[4 * y + 3]);
+  } else {
+#pragma unroll
+    for (int y = 0; y < 4; y++)
+#pragma unroll
+      for (int x = 0; x < 4; x++) {
+        int b = 4 * y + x;
+        inv_lift(q[b + 0], q[b + 16], q[b + 32], q[b + 48]);
+      }
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+      for (int z = 0; z < 4; z++) {
+        int b = 16 * z + x;
+        inv_lift(q[b + 0], q[b + 4], q[b + 8], q[b + 12]);
+      }
+#pragma unroll
+    for (int z = 0; z < 4; z++)
+#pragma unroll
+      for (int y = 0; y < 4; y++) {
+        int b = 16 * z + 4 * y;
+        inv_lift(q[b + 0], q[b + 1], q[b + 2], q[b + 3]);
+      }
+  }
+}
+
+// twoscomplement_to_negabinary + fwd_reorder_int2uint (encode.c:263-275), static permutation.
+template <int D>
+__device__ __forceinline__ void fwd_reorder(uint32_t* u, const int32_t* q)
+{
+  constexpr int B = Dim<D>::B;
+#pragma unroll
+  for (int i = 0; i < B; i++) u[i] = ((uint32_t)q[perm_index(D, i)] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+}
+
+// negabinary_to_twoscomplement + bwd_reorder_uint2int (decode.c:44-56)
+template <int D>
+__device__ __forceinline__ void inv_reorder(int32_t* q, const uint32_t* u)
+{
+  constexpr int B = Dim<D>::B;
+#pragma unroll
+  for (int i = 0; i < B; i++) q[perm_index(D, i)] = (int32_t)((u[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+}
+
+// Bit plane k of B coefficients: bit i of the result = bit k of u[i] (encode.c:295-299).
+template <int B>
+__device__ __forceinline__ typename PlaneType<B>::T get_plane(const uint32_t* u, int k)
+{
+  using PT = typename PlaneType<B>::T;
+  PT x = 0;
+#pragma unroll
+  for (int i = 0; i < B; i++) x |= (PT)((u[i] >> k) & 1u) << i;
+  return x;
+}
+
+// ------------------------------------------------------------------------------------------------ writers
+// A writer appends bits LSB-first; put(v, n) requires v < 2^n (n <= 64), skip(n) appends zeros.
+// Every writer truncates at its limit, which makes the untruncated coder below equal the budgeted one.
+
+// Count-only writer (bit lengths for variable-rate offsets).
+struct CountWriter {
+  __device__ __forceinline__ void put(uint64_t, uint32_t) {}
+  __device__ __forceinline__ void skip(uint32_t) {}
+};
+
+// Up to 64 bits in one register (fixed-rate blocks of <= 64 bits).
+struct RegWriter64 {
+  uint64_t acc;
+  uint32_t pos;
+  __device__ __forceinline__ void put(uint64_t v, uint32_t n)
+  {
+    if (pos < 64) acc |= v << pos;
+    pos += n;
+  }
+  __device__ __forceinline__ void skip(uint32_t n) { pos += n; }
+};
+
+// Bits OR-ed into a zero-initialised LDS window of 32-bit words at a local bit offset.
+struct LdsWriter {
+  uint32_t* lds;
+  uint32_t pos, limit;
+  __device__ __forceinline__ void put(uint64_t v, uint32_t n)
+  {
+    if (pos >= limit || n == 0) { pos += n; return; }
+    uint32_t room = limit - pos;
+    if (n > room) v &= lowmask64(room);
+    uint32_t w = pos >> 5, sh = pos & 31;
+    uint32_t p0 = (uint32_t)(v << sh);
+    uint32_t p1 = (uint32_t)((v << sh) >> 32);
+    uint32_t p2 = sh ? (uint32_t)(v >> (64 - sh)) : 0u;
+    if (p0) atomicOr(&lds[w], p0);
+    if (p1) atomicOr(&lds[w + 1], p1);
+    if (p2) atomicOr(&lds[w + 2], p2);
+    pos += n;
+  }
+  __device__ __forceinline__ void skip(uint32_t n) { pos += n; }
+};
+
+// ------------------------------------------------------------------------------------------------ coder
+// encode_partial_bitplanes / encode_all_bitplanes (encode.c:279-408). Emits the untruncated plane codes until the
+// budget is consumed; returns min(untruncated bits, budget) = what the budgeted coder writes.
+template <int B, class W>
+__device__ __forceinline__ uint32_t encode_ints(W& w, const uint32_t* u, uint32_t budget, uint32_t maxprec)
+{
+  using PT = typename PlaneType<B>::T;
+  const int kmin = maxprec < 32 ? 32 - (int)maxprec : 0;
+  uint32_t bits = 0;
+  uint32_t n = 0;
+  for (int k = 31; k >= kmin && bits < budget; --k) {
+    PT x = get_plane<B>(u, k);
+    // step 2: first n bits verbatim
+    w.put((uint64_t)x & lowmask64(n), n);
+    bits += n;
+    PT r = n < (uint32_t)B ? (PT)(x >> n) : (PT)0;
+    // step 3: unary run-length (group test) code of the remainder
+    while (n < (uint32_t)B && bits < budget) {
+      if (r == 0) {  // negative group test: done with this plane
+        w.skip(1);
+        bits += 1;
+        break;
+      }
+      uint32_t t = (B == 64) ? (uint32_t)__builtin_ctzll((uint64_t)r) : (uint32_t)__builtin_ctz((uint32_t)r);
+      if (n + t < (uint32_t)B - 1) {  // group '1', t zeros, the one-bit
+        w.put(1ull | (2ull << t), t + 2);
+        bits += t + 2;
+        n += t + 1;
+        r = (PT)(r >> (t + 1));
+      } else {  // the one-bit sits in the last position and is implied
+        w.put(1ull, 1);
+        w.skip(B - 1 - n);
+        bits += B - n;
+        n = B;
+      }
+    }
+  }
+  return bits < budget ? bits : budget;
+}
+
+__device__ __forceinline__ bool exceeded_maxbits(uint32_t maxbits, uint32_t maxprec, uint32_t size)
+{
+  return (maxprec + 1) * size - 1 > maxbits;  // common.c:232-236
+}
+
+// encode_fblock (encode.c:457-495) + encode_iblock (encode.c:412-455). Returns the block's bit count.
+template <int D, class W>
+__device__ __forceinline__ uint32_t encode_block(W& w, const float* f, const Params& p)
+{
+  constexpr int B = Dim<D>::B;
+  float fa[B];
+#pragma unroll
+  for (int i = 0; i < B; i++) fa[i] = f[i];
+  const int emax = block_emax<B>(fa);
+  const uint32_t prec = precision(emax, p.maxprec, p.minexp, D);
+  const uint32_t be = prec ? (uint32_t)(emax + 127) : 0u;
+  if (!be) {  // single zero bit, then pad to minbits
+    w.skip(1);
+    uint32_t bits = 1;
+    if (p.minbits > bits) {
+      w.skip(p.minbits - bits);
+      bits = p.minbits;
+    }
+    return bits;
+  }
+  w.put(2ull * be + 1ull, 9);
+  int32_t q[B];
+  const float s = cast_scale(emax);
+#pragma unroll
+  for (int i = 0; i < B; i++) q[i] = cast1(fa[i], s);
+  fwd_xform<D>(q);
+  uint32_t u[B];
+  fwd_reorder<D>(u, q);
+  const uint32_t maxb = p.maxbits - 9u;
+  const uint32_t minb = p.minbits - (p.minbits < 9u ? p.minbits : 9u);
+  const uint32_t budget = exceeded_maxbits(maxb, prec, B) ? maxb : 0xffffffffu;
+  uint32_t bits = encode_ints<B>(w, u, budget, prec);
+  if (bits < minb) {
+    w.skip(minb - bits);
+    bits = minb;
+  }
+  return 9 + bits;
+}
+
+// ------------------------------------------------------------------------------------------------ reader / decoder
+struct BitReader {
+  const uint64_t* w;
+  uint64_t pos;
+  __device__ __forceinline__ uint64_t peek64() const
+  {
+    uint64_t i = pos >> 6;
+    uint32_t sh = (uint32_t)(pos & 63);
+    uint64_t v = w[i] >> sh;
+    if (sh) v |= w[i + 1] << (64 - sh);
+    return v;
+  }
+  __device__ __forceinline__ uint64_t get(uint32_t n)
+  {
+    if (!n) return 0;
+    uint64_t v = peek64() & lowmask64(n);
+    pos += n;
+    return v;
+  }
+  __device__ __forceinline__ uint32_t bit()
+  {
+    uint32_t b = (uint32_t)(w[pos >> 6] >> (pos & 63)) & 1u;
+    pos++;
+    return b;
+  }
+};
+
+// decode_ints (libzfp 0.5.5; sw/src/decode.c:141-183 with block size 4^d)
+template <int B>
+__device__ __forceinline__ uint32_t decode_ints(BitReader& r, uint32_t maxbits, uint32_t maxprec, uint32_t* u)
+{
+  const int kmin = maxprec < 32 ? 32 - (int)maxprec : 0;
+  uint32_t bits = maxbits;
+  uint32_t n = 0;
+#pragma unroll
+  for (int i = 0; i < B; i++) u[i] = 0;
+  for (int k = 31; bits && k >= kmin; --k) {
+    uint32_t m = n < bits ? n : bits;
+    bits -= m;
+    uint64_t x = r.get(m);
+    for (; n < (uint32_t)B && bits && (bits--, r.bit()); x += 1ull << n++)
+      for (; n < (uint32_t)B - 1 && bits && (bits--, !r.bit()); n++)
+        ;
+#pragma unroll
+    for (int i = 0; i < B; i++) u[i] += (uint32_t)((x >> i) & 1u) << k;
+  }
+  return maxbits - bits;
+}
+
+// dequantize (decode.c:12-25): ldexpf(1, emax - 30) exactly, including subnormal and zero scales.
+__device__ __forceinline__ float dequant_scale(int emax)
+{
+  int e = emax - 30;
+  if (e >= -126) return __uint_as_float((uint32_t)(e + 127) << 23);
+  if (e >= -149) return __uint_as_float(1u << (e + 149));
+  return 0.0f;
+}
+
+// decode_fblock (decode.c:220-253 with libzfp semantics). Writes B floats to f.
+template <int D>
+__device__ __forceinline__ void decode_block(BitReader& r, const Params& p, float* f)
+{
+  constexpr int B = Dim<D>::B;
+  uint32_t bits = 1;
+  if (r.bit()) {
+    bits += 8;
+    const int emax = (int)r.get(8) - 127;
+    const uint32_t prec = precision(emax, p.maxprec, p.minexp, D);
+    const uint32_t minb = p.minbits - (p.minbits < bits ? p.minbits : bits);
+    const uint32_t maxb = p.maxbits - bits;
+    uint32_t u[B];
+    const uint32_t budget = exceeded_maxbits(maxb, prec, B) ? maxb : 0xffffffffu;
+    uint32_t got = decode_ints<B>(r, budget, prec, u);
+    if (got < minb) r.pos += minb - got;
+    int32_t q[B];
+    inv_reorder<D>(q, u);
+    inv_xform<D>(q);
+    const float s = dequant_scale(emax);
+#pragma unroll
+    for (int i = 0; i < B; i++) f[i] = s * (float)q[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < B; i++) f[i] = 0.0f;
+    if (p.minbits > bits) r.pos += p.minbits - bits;
+  }
+}
+
+}  // namespace gcow

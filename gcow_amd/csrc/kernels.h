@@ -1,0 +1,46 @@
+// kernels.h -- host-visible kernel launch interface (internal to libgcow.so).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "codec_device.h"
+
+namespace gcow {
+
+// Field geometry as the kernels see it: extents/strides fastest-first, unused dims have extent 1.
+struct FieldDesc {
+  const void* data;  // input (encode) or output (decode) device pointer
+  uint64_t n[3];
+  int64_t s[3];
+  uint32_t bx, by, bz;
+  uint32_t nblocks;
+  uint32_t dims;
+  uint32_t dtype;
+  uint32_t vec;  // rows of 4 values are contiguous and vector-aligned
+};
+
+// Workgroup range decomposition for the tile kernels.
+struct TilePlan {
+  uint32_t threads;    // blocks per tile (= workgroup size)
+  uint32_t range;      // blocks per workgroup range (multiple of threads)
+  uint32_t nranges;    // grid size
+  uint32_t lds_words;  // LDS window (32-bit words)
+  bool fixed;          // minbits == maxbits: offsets are b * maxbits
+};
+
+hipError_t launch_encode_fixed1d(const void* in, int dtype, uint64_t nvals, uint32_t nblocks, const Params& p,
+                                 void* out, void* stream);
+hipError_t launch_encode_tiles(const FieldDesc& F, const Params& p, const TilePlan& plan, uint32_t* out32,
+                               uint64_t* ws_sums, uint64_t* ws_base, uint64_t* d_total, uint64_t* index,
+                               uint32_t index_shift, void* stream);
+hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
+                         uint32_t chunk, uint64_t nchunks, bool fixed, uint64_t base_bits, uint64_t* end_out,
+                         void* stream);
+hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
+hipError_t launch_stitch(uint64_t* dst, uint64_t off, const uint64_t* src, uint64_t bits, void* stream);
+hipError_t launch_stage(int which, int dims, const void* a, const void* b, uint32_t n, void* out, uint32_t x0,
+                        uint32_t x1, void* out2, uint32_t slot_words, void* stream);
+hipError_t launch_fill_normal(float* out, uint64_t count, double sigma, uint64_t seed, int inject, void* stream);
+
+}  // namespace gcow

@@ -1,0 +1,264 @@
+/*
+ * gcow.h -- MI355X-native ZFP-style gradient codec: the C ABI (libgcow.so).
+ *
+ * Part 1 is the drop-in boundary: the reference's sw/ encoder/decoder call surface with the same type layouts,
+ * names, argument meaning and return values (fpgasystems/gcow sw/include/{types,zfp,stream,common}.h), each
+ * declaration citing the reference interface it replaces. The codec behind it runs as hand-written CDNA4 (gfx950)
+ * HIP kernels; there is no CPU codec in libgcow.so.
+ *
+ * Part 2 is the device API the drop-in layer is built on: device pointers, an explicit hipStream_t (passed as
+ * void*), explicit status codes. No torch/HIP types appear in any signature.
+ *
+ * Deviations from sw/ (all documented in INTEGRATION.md):
+ *   - 1-D (dim = 1) and 3-D inputs are supported (sw/ only encodes 2-D: sw/src/zfp.c:12-24, common.c:122-125).
+ *   - data may be a device pointer; it is then encoded in place on the GPU. free_zfp_input() frees host data
+ *     exactly as sw/ does (sw/src/common.c:54-62) but never frees device memory it does not own.
+ *   - zfp_decompress() decodes with libzfp 0.5.5 semantics (block size 4^d); sw/'s decoder passes dim where the
+ *     block size is needed (sw/src/decode.c:193-202) and is not reproduced.
+ *   - dtype_bf16 (extension): bf16 values are widened exactly to fp32 and coded by the fp32 codec.
+ *   - the library never prints (sw/src/common.c:109,190,193 do).
+ */
+#ifndef GCOW_H
+#define GCOW_H
+
+#include <stdarg.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ================================================================================================
+ * Part 1 -- drop-in sw/ surface
+ * ============================================================================================== */
+
+/* sw/include/types.h:8-21 */
+typedef unsigned char uchar;
+typedef unsigned short ushort;
+typedef unsigned int uint;
+typedef unsigned long ulong;
+typedef int8_t int8;
+typedef uint8_t uint8;
+typedef int16_t int16;
+typedef uint16_t uint16;
+typedef int32_t int32;
+typedef uint32_t uint32;
+typedef int64_t int64;
+typedef uint64_t uint64;
+
+/* sw/include/types.h:24 -- 64-bit stream words, bits appended LSB-first, words little-endian */
+typedef uint64 stream_word;
+
+/* sw/include/types.h:29-36 */
+typedef enum {
+  zfp_null = 0,
+  zfp_expert = 1,
+  zfp_fixed_rate = 2,
+  zfp_fixed_precision = 3,
+  zfp_fixed_accuracy = 4,
+  zfp_reversible = 5
+} zfp_mode;
+
+/* sw/include/types.h:39-45 (+ dtype_bf16 extension) */
+typedef enum {
+  dtype_none = 0,
+  dtype_int32 = 1,
+  dtype_int64 = 2,
+  dtype_float = 3,
+  dtype_double = 4,
+  dtype_bf16 = 5
+} data_type;
+
+/* sw/include/types.h:51-56 -- zero extents for unused dimensions, zero stride = contiguous a[nw][nz][ny][nx] */
+typedef struct {
+  data_type dtype;
+  void* data;
+  size_t nx, ny, nz, nw;
+  ptrdiff_t sx, sy, sz, sw;
+} zfp_input;
+
+/* sw/include/stream.h:6-16 */
+typedef struct stream stream;
+struct stream {
+  size_t buffered_bits;
+  stream_word buffer;
+  stream_word* begin;
+  ptrdiff_t idx;
+  ptrdiff_t end;
+};
+
+/* sw/include/types.h:58-65 */
+typedef struct {
+  uint minbits;
+  uint maxbits;
+  uint maxprec;
+  int minexp;
+  stream* data;
+} zfp_output;
+
+/* sw/include/common.h:10-13 */
+#define ZFP_MIN_BITS 1
+#define ZFP_MAX_BITS 16658
+#define ZFP_MAX_PREC 64
+#define ZFP_MIN_EXP -1074
+#define ZFP_HEADER_MAX_BITS 148
+
+/* ---- parameters / descriptors (sw/include/types.h:107-121, sw/src/common.c) ---- */
+double set_zfp_output_accuracy(zfp_output* output, double tolerance);      /* common.c:6-21 */
+zfp_input* alloc_zfp_input(void);                                           /* common.c:26-36 */
+zfp_output* alloc_zfp_output(void);                                         /* common.c:41-52 */
+void free_zfp_input(zfp_input* input);                                      /* common.c:54-62 */
+void free_zfp_output(zfp_output* output);                                   /* common.c:64-75 */
+void cleanup(zfp_input* input, zfp_output* output);                         /* common.c:77-81 */
+zfp_input* init_zfp_input(void* data, data_type dtype, uint dim, ...);     /* common.c:83-103 (dim 1 added) */
+zfp_output* init_zfp_output(const zfp_input* input);                        /* common.c:105-115 */
+uint is_reversible(const zfp_output* output);                               /* common.c:117-120 */
+uint get_input_dimension(const zfp_input* input);                           /* common.c:122-125 (1-D added) */
+size_t get_input_num_blocks(const zfp_input* input);                        /* common.c:127-143 */
+size_t get_input_size(const zfp_input* input, size_t* shape);               /* common.c:145-164 */
+size_t get_dtype_size(data_type dtype);                                     /* common.c:166-180 */
+uint get_input_precision(const zfp_input* input);                           /* common.c:182-185 */
+size_t get_max_output_bytes(const zfp_output* output, const zfp_input* input); /* common.c:187-224 */
+uint get_precision(int maxexp, uint maxprec, int minexp, int dim);          /* common.c:226-229 */
+int exceeded_maxbits(uint maxbits, uint maxprec, uint size);                /* common.c:232-236 */
+
+/* Extensions: the other libzfp 0.5.5 parameter setters (the Python caller uses rate / precision / accuracy,
+ * hw/models/train_imagenet.py:459-464). */
+double set_zfp_output_rate(zfp_output* output, double rate, uint dim);
+uint set_zfp_output_precision(zfp_output* output, uint precision);
+int set_zfp_output_expert(zfp_output* output, uint minbits, uint maxbits, uint maxprec, int minexp);
+
+/* ---- array codec (sw/include/zfp.h:4-7, sw/src/zfp.c) ---- */
+size_t zfp_compress(zfp_output* output, const zfp_input* input);            /* zfp.c:10-28 */
+size_t zfp_decompress(zfp_output* output, const zfp_input* input);          /* zfp.c:58-76 */
+
+/* ---- bit stream (sw/include/stream.h:18-33, sw/src/stream.c) ---- */
+stream* stream_init(void* buffer, size_t bytes);                            /* stream.c:160-169 */
+void stream_rewind(stream* s);                                              /* stream.c:153-158 */
+size_t stream_size_bytes(const stream* s);                                  /* stream.c:176-179 */
+size_t stream_flush(stream* s);                                             /* stream.c:132-138 */
+uint64 stream_woffset(stream* s);                                           /* stream.c:141-144 */
+uint64 stream_roffset(stream* s);                                           /* stream.c:147-150 */
+void stream_pad(stream* s, uint64 n);                                       /* stream.c:121-129 */
+stream_word stream_read_word(stream* s);                                    /* stream.c:6-15 */
+void stream_write_word(stream* s, stream_word value);                       /* stream.c:18-26 */
+uint64 stream_read_bits(stream* s, size_t n);                               /* stream.c:29-58 */
+uint64 stream_write_bits(stream* s, uint64 value, size_t n);                /* stream.c:61-92 */
+uint stream_read_bit(stream* s);                                            /* stream.c:95-106 */
+uint stream_write_bit(stream* s, uint bit);                                 /* stream.c:109-118 */
+void stream_rseek(stream* s, uint64 offset);                                /* stream.c:182-197 */
+void stream_skip(stream* s, uint64 n);                                      /* stream.c:200-203 */
+size_t stream_algin_next_word(stream* s);                                   /* stream.c:206-211 */
+
+/* ---- block API (sw/include/encode.h:17-81, decode.h:8-12), batched onto the GPU stage kernels ---- */
+void gather_2d_block(float* block, const float* raw, ptrdiff_t sx, ptrdiff_t sy);            /* encode.c:62-70 */
+void gather_partial_2d_block(float* block, const float* raw, size_t nx, size_t ny, ptrdiff_t sx,
+                             ptrdiff_t sy);                                                   /* encode.c:72-88 */
+void gather_4d_block(float* block, const float* raw, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz,
+                     ptrdiff_t sw);                                                           /* encode.c:90-99 */
+void gather_partial_4d_block(float* block, const float* raw, size_t nx, size_t ny, size_t nz, size_t nw,
+                             ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);        /* encode.c:101-126 */
+int get_scaler_exponent(float x);                                           /* encode.c:128-140 */
+int get_block_exponent(const float* block, uint n);                         /* encode.c:142-152 */
+void fwd_cast_block(int32* iblock, const float* fblock, uint n, int emax); /* encode.c:178-187 */
+void fwd_decorrelate_2d_block(int32* iblock);                               /* encode.c:251-260 */
+void fwd_reorder_int2uint(uint32* ublock, const int32* iblock, const uchar* perm, uint n); /* encode.c:269-275 */
+uint encode_all_bitplanes(stream* const s, const uint32* const ublock, uint maxprec, uint block_size);
+                                                                            /* encode.c:343-408 */
+uint encode_partial_bitplanes(stream* const s, const uint32* const ublock, uint maxbits, uint maxprec,
+                              uint block_size);                             /* encode.c:279-339 */
+uint encode_iblock(stream* const out_data, uint minbits, uint maxbits, uint maxprec, int32* iblock,
+                   size_t dim);                                             /* encode.c:412-455 */
+uint encode_fblock(zfp_output* output, const float* fblock, size_t dim);   /* encode.c:457-495 */
+uint decode_fblock(zfp_output* output, float* fblock, size_t dim);         /* decode.c:220-253 */
+void scatter_2d_block(const float* block, float* raw, ptrdiff_t sx, ptrdiff_t sy);           /* decode.c:27-34 */
+void scatter_partial_2d_block(const float* block, float* raw, size_t nx, size_t ny, ptrdiff_t sx,
+                              ptrdiff_t sy);                                                  /* decode.c:36-42 */
+
+/* PERM_2D (sw/include/types.h:71-97) is exported as data for fwd_reorder_int2uint callers. */
+extern const uchar PERM_2D[16];
+
+/* ================================================================================================
+ * Part 2 -- device API (what the drop-in layer and the Python/torch host binding call)
+ * ============================================================================================== */
+
+typedef enum {
+  GCOW_OK = 0,
+  GCOW_ERR_INVALID = 1,     /* bad arguments / parameters */
+  GCOW_ERR_CAPACITY = 2,    /* output buffer smaller than the bound gcow_max_output_bytes() */
+  GCOW_ERR_HIP = 3,         /* a HIP runtime call failed (gcow_last_error() has the text) */
+  GCOW_ERR_NODEVICE = 4,    /* no gfx950 device / kernels not loadable */
+  GCOW_ERR_UNSUPPORTED = 5  /* valid but not supported (e.g. int32/int64/double dtypes) */
+} gcow_status;
+
+/* The four ZFP expert parameters (sw/include/types.h:58-62). */
+typedef struct {
+  uint minbits, maxbits, maxprec;
+  int minexp;
+} gcow_params;
+
+const char* gcow_status_string(gcow_status s);
+const char* gcow_last_error(void);
+const char* gcow_version(void);
+
+/* Upper bound on the flushed stream for `field` under `p` (the sw/ bound without the 148-bit header term). */
+size_t gcow_max_output_bytes(const zfp_input* field, const gcow_params* p);
+/* Device scratch needed by gcow_encode_device (variable-rate passes); 0 for fixed rate. */
+size_t gcow_encode_workspace_bytes(const zfp_input* field, const gcow_params* p);
+/* Number of uint64 entries of the block-offset index written with `index_stride` (0 = no index). */
+size_t gcow_index_entries(const zfp_input* field, uint32_t index_stride);
+
+/*
+ * Encode field->data (DEVICE pointer, fp32 or bf16, 1-3 dims, any element strides) into d_out (device).
+ * The stream is byte-identical to sw/'s zfp_compress on the same values (headerless, LSB-first 64-bit words,
+ * flushed with zero bits to a 64-bit boundary). *d_total_bits (device uint64, may be NULL) receives the unflushed
+ * bit count. d_index (device, may be NULL) receives the bit offset of every index_stride-th block (1..256, power of
+ * two), which gcow_decode_device uses to decode variable-rate streams in parallel.
+ * Asynchronous with respect to the host on hip_stream (NULL = default stream); no host synchronisation.
+ */
+gcow_status gcow_encode_device(const zfp_input* field, const gcow_params* p, void* d_out, size_t out_capacity,
+                               uint64_t* d_total_bits, void* d_workspace, size_t workspace_bytes,
+                               uint64_t* d_index, uint32_t index_stride, void* hip_stream);
+
+/*
+ * Decode d_in into field->data (DEVICE fp32 pointer) with libzfp 0.5.5 semantics. Fixed-rate streams
+ * (minbits == maxbits) decode one block per thread; variable-rate streams need the index written by
+ * gcow_encode_device (d_index/index_stride), or, with d_index == NULL, are decoded by a single sequential GPU lane.
+ */
+gcow_status gcow_decode_device(const zfp_input* field, const gcow_params* p, const void* d_in, size_t in_bytes,
+                               const uint64_t* d_index, uint32_t index_stride, void* hip_stream);
+
+/*
+ * Bit-stitch for sharded variable-rate streams: OR `src_bits` bits of d_src into d_dst starting at bit
+ * `dst_bit_offset` (d_dst words covering the target range must be zero beyond what earlier shards wrote).
+ * Used after an all-gather of per-rank shard streams to rebuild the single-stream sw/ layout.
+ */
+gcow_status gcow_stitch_device(uint64_t* d_dst, uint64_t dst_bit_offset, const uint64_t* d_src, uint64_t src_bits,
+                               void* hip_stream);
+
+/* Per-stage batched device kernels (the hw/stages split, for parity bisection; sw/tests/test_stages.cpp). */
+gcow_status gcow_stage_emax_device(const float* d_blocks, uint32_t nblocks, uint32_t dims, int32_t* d_emax,
+                                   void* hip_stream);
+gcow_status gcow_stage_cast_device(const float* d_blocks, const int32_t* d_emax, uint32_t nblocks, uint32_t dims,
+                                   int32_t* d_iblocks, void* hip_stream);
+gcow_status gcow_stage_xform_device(int32_t* d_iblocks, uint32_t nblocks, uint32_t dims, int inverse,
+                                    void* hip_stream);
+gcow_status gcow_stage_reorder_device(const int32_t* d_iblocks, uint32_t nblocks, uint32_t dims,
+                                      uint32_t* d_ublocks, void* hip_stream);
+/* Embedded coder on one ublock per lane, each into its own zeroed slot of slot_words words after `header_bits`
+ * bits of header (value header); bits written per block to d_bits. */
+gcow_status gcow_stage_encode_ints_device(const uint32_t* d_ublocks, uint32_t nblocks, uint32_t dims,
+                                          uint32_t budget, uint32_t maxprec, uint64_t* d_slots, uint32_t slot_words,
+                                          uint32_t* d_bits, void* hip_stream);
+
+/* Deterministic synthetic gradient bucket on the device (bench / smoke inputs; SURVEY 8(d) distribution):
+ * N(0, sigma) via counter-based splitmix64 + Box-Muller, with zero / tiny / subnormal 4-value blocks injected at
+ * 1/64, 1/4096, 1/4096. */
+gcow_status gcow_fill_normal_device(float* d_out, size_t count, double sigma, uint64_t seed, int inject,
+                                    void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GCOW_H */

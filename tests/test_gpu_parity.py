@@ -1,0 +1,414 @@
+"""GPU parity: the HIP codec (through the C ABI) against the pinned oracle and fixtures. Bit-exact everywhere.
+
+Sizes: fixtures/goldens as the reference holds them; random cases the oracle finishes in well under a second; the
+BASELINE configs at full size (256 Mi fp32 1-D fixed rate, 512^3 3-D round trip) against the threaded oracle.
+"""
+import ctypes as C
+import hashlib
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def gc():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a device")
+    from gcow_amd import codec
+    return codec
+
+
+def P(gc, orc_params):
+    return gc.expert(*orc_params.tuple())
+
+
+def dev_encode_bytes(gc, arr, params, index_stride=0):
+    x = torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+    if arr.dtype == np.uint16:
+        x = x.view(torch.bfloat16)
+    e = gc.encode(x, params, index_stride=index_stride)
+    torch.cuda.synchronize()
+    return e, e.to_bytes()
+
+
+# ---------------------------------------------------------------------------------------------- reference goldens
+GOLDENS = json.load(open(os.path.join(GOLD, "reference_goldens.json")))["goldens"]
+
+
+@pytest.mark.parametrize("g", GOLDENS, ids=lambda g: g["file"])
+def test_reference_goldens_device(gc, orc, g):
+    a = orc.gen_bump2d(g["n"], g["recipe"] == "bump_f32sum")
+    _, b = dev_encode_bytes(gc, a, gc.accuracy(g["tolerance"]))
+    assert len(b) == g["bytes"]
+    assert _sha(b) == g["sha256"]
+
+
+# ---------------------------------------------------------------------------------------------- libzfp fixtures
+FX = json.load(open(os.path.join(GOLD, "libzfp_fixtures.json")))["cases"]
+
+
+@pytest.fixture(scope="module")
+def fxa():
+    return np.load(os.path.join(GOLD, "libzfp_fixtures.npz"))
+
+
+@pytest.mark.parametrize("c", FX, ids=lambda c: c["name"])
+def test_libzfp_fixture_device(gc, fxa, c):
+    a = fxa["input__" + c["input"]]
+    p = gc.expert(*c["params"])
+    stride = 4 if len(a.shape) < 3 else 1
+    e, b = dev_encode_bytes(gc, a, p, index_stride=0 if gc.is_fixed(p) else stride)
+    assert len(b) == c["bytes"]
+    assert _sha(b) == c["stream_sha256"]
+    d = gc.decode(e)
+    torch.cuda.synchronize()
+    assert _sha(d.cpu().numpy().tobytes()) == c["decoded_sha256"]
+
+
+@pytest.mark.parametrize("c", [c for c in FX if c["mode"] in ("acc", "prec", "expert")][::7], ids=lambda c: c["name"])
+def test_sequential_decode_without_index(gc, fxa, c):
+    """A foreign variable-rate stream (no block index) decodes on one sequential GPU lane."""
+    a = fxa["input__" + c["input"]]
+    p = gc.expert(*c["params"])
+    words = torch.from_numpy(fxa[c["name"] + "__stream"].view(np.int64).copy()).cuda()
+    words = torch.cat([words, torch.zeros(2, dtype=torch.int64, device="cuda")])
+    d = gc.decode(words, a.shape, p)
+    torch.cuda.synchronize()
+    assert _sha(d.cpu().numpy().tobytes()) == c["decoded_sha256"]
+
+
+# ---------------------------------------------------------------------------------------------- random vs oracle
+def _check_vs_oracle(gc, orc, a, op, index_stride=0, decode=True):
+    w_ref, bits_ref = orc.compress(a, op)
+    e, b = dev_encode_bytes(gc, a, P(gc, op), index_stride)
+    assert e.bits == bits_ref
+    assert b == w_ref.tobytes()
+    if decode:
+        ref = orc.decompress(w_ref, a.shape, op)
+        d = gc.decode(e)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 8, 255, 1023, 4097, (1 << 18) + 3])
+@pytest.mark.parametrize("r", [16, 8])
+def test_fast1d_fixed_rate(gc, orc, n, r):
+    a = orc.gen_normal(n, 1e-3, 0x1234 + n, True)
+    _check_vs_oracle(gc, orc, a, orc.rate(r, 1))
+
+
+@pytest.mark.parametrize("r", [4, 2.5, 32, 12])
+def test_1d_other_rates(gc, orc, r):
+    a = orc.gen_normal(10007, 1e-3, 99, True)
+    _check_vs_oracle(gc, orc, a, orc.rate(r, 1))
+
+
+@pytest.mark.parametrize("shape", [(1000,), (4096 * 3 + 1,), (37, 53), (64, 64), (9, 10, 7), (16, 20, 24)])
+@pytest.mark.parametrize("mode", ["acc3", "acc6", "prec12", "rate8", "expert"])
+def test_random_all_dims(gc, orc, shape, mode):
+    rng = np.random.default_rng(zlib.crc32(repr((shape, mode)).encode()))
+    a = (rng.standard_normal(shape) * 1e-2).astype(np.float32)
+    flat = a.reshape(-1)
+    flat[:: 97] = 0
+    flat[5:9] = [1e-36, -2e-38, 7e-39, 0]  # tiny and subnormal members
+    op = {"acc3": orc.accuracy(1e-3), "acc6": orc.accuracy(1e-6), "prec12": orc.precision(12),
+          "rate8": orc.rate(8, len(shape)), "expert": orc.expert(20, 160, 20, -30)}[mode]
+    _check_vs_oracle(gc, orc, a, op, index_stride=0 if op.minbits == op.maxbits else 2)
+
+
+def test_subnormal_cast_members(gc, orc):
+    """Blocks with emax in [-97, -90] whose members are subnormal: the cast must not flush them."""
+    rng = np.random.default_rng(5)
+    blocks = []
+    for e in range(-97, -89):
+        for _ in range(64):
+            v = rng.standard_normal(4) * (2.0 ** e)
+            v[rng.integers(0, 4)] = rng.standard_normal() * 2.0 ** -127
+            v[rng.integers(0, 4)] = 2.0 ** -149 * rng.integers(1, 100)
+            blocks.append(v)
+    a = np.array(blocks, np.float32).reshape(-1)
+    for op in (orc.rate(16, 1), orc.accuracy(1e-40), orc.precision(32)):
+        _check_vs_oracle(gc, orc, a, op, index_stride=0 if op.minbits == op.maxbits else 1)
+
+
+@pytest.mark.parametrize("mode", ["rate16", "rate8", "acc6", "acc3"])
+def test_bf16(gc, orc, mode):
+    f = orc.gen_normal(50001, 1e-3, 7, True)
+    bf = (f.view(np.uint32) >> 16).astype(np.uint16)  # truncation is as good as any bf16 input
+    op = {"rate16": orc.rate(16, 1), "rate8": orc.rate(8, 1), "acc6": orc.accuracy(1e-6),
+          "acc3": orc.accuracy(1e-3)}[mode]
+    _check_vs_oracle(gc, orc, bf, op, index_stride=0 if op.minbits == op.maxbits else 8, decode=False)
+
+
+def test_strided_views(gc, orc):
+    rng = np.random.default_rng(3)
+    base = (rng.standard_normal((40, 66)) * 1e-3).astype(np.float32)
+    x = torch.from_numpy(base).cuda()
+    for view, ref in [(x.t(), base.T), (x[:, ::2], base[:, ::2]), (x[3:35, 5:60], base[3:35, 5:60]),
+                      (x.reshape(-1)[1::3], base.reshape(-1)[1::3])]:
+        for op in (orc.accuracy(1e-4), orc.rate(8, len(ref.shape))):
+            w_ref, bits = orc.compress(np.ascontiguousarray(ref), op)
+            e = gc.encode(view, P(gc, op))
+            torch.cuda.synchronize()
+            assert e.bits == bits and e.to_bytes() == w_ref.tobytes()
+
+
+def test_empty_and_tiny(gc, orc):
+    for n in (1, 2, 3):
+        a = np.array([1.5, -2.0, 3.25][:n], np.float32)
+        _check_vs_oracle(gc, orc, a, orc.accuracy(1e-3))
+        _check_vs_oracle(gc, orc, a, orc.rate(16, 1))
+
+
+# ---------------------------------------------------------------------------------------------- stitch (multi-GPU)
+@pytest.mark.parametrize("k", [2, 3, 8])
+def test_stitch_equals_single_stream(gc, orc, k):
+    a = orc.gen_normal(4 * 10001, 1e-3, 11, True)
+    op = orc.accuracy(1e-6)
+    w_ref, bits_ref = orc.compress(a, op)
+    nb = len(a) // 4
+    cuts = [4 * (nb * i // k) for i in range(k + 1)]
+    out = torch.zeros((bits_ref + 63) // 64 + 1, dtype=torch.int64, device="cuda")
+    off = 0
+    for i in range(k):
+        e, _ = dev_encode_bytes(gc, a[cuts[i]:cuts[i + 1]], P(gc, op))
+        gc.stitch(out, off, e.words, e.bits)
+        off += e.bits
+    torch.cuda.synchronize()
+    assert off == bits_ref
+    assert out[: (bits_ref + 63) // 64].cpu().numpy().tobytes() == w_ref.tobytes()
+
+
+# ---------------------------------------------------------------------------------------------- stage kernels
+def test_stage_kernels(gc, orc):
+    from gcow_amd import _ffi
+    L = _ffi.load()
+    rng = np.random.default_rng(2)
+    for dims in (1, 2, 3):
+        B = 4 ** dims
+        nb = 300
+        f = (rng.standard_normal((nb, B)) * 10.0 ** rng.integers(-40, 30, (nb, 1))).astype(np.float32)
+        f[0, :3] = [np.nan, np.inf, 1e-40]
+        df = torch.from_numpy(f).cuda()
+        de = torch.zeros(nb, dtype=torch.int32, device="cuda")
+        _ffi.check(L.gcow_stage_emax_device(df.data_ptr(), nb, dims, de.data_ptr(), None))
+        dq = torch.zeros((nb, B), dtype=torch.int32, device="cuda")
+        _ffi.check(L.gcow_stage_cast_device(df.data_ptr(), de.data_ptr(), nb, dims, dq.data_ptr(), None))
+        torch.cuda.synchronize()
+        em = de.cpu().numpy()
+        q = dq.cpu().numpy()
+        for i in range(nb):
+            assert em[i] == orc.block_exponent(f[i])
+            assert np.array_equal(q[i], orc.fwd_cast(f[i], int(em[i])))
+        _ffi.check(L.gcow_stage_xform_device(dq.data_ptr(), nb, dims, 0, None))
+        du = torch.zeros((nb, B), dtype=torch.int32, device="cuda")
+        _ffi.check(L.gcow_stage_reorder_device(dq.data_ptr(), nb, dims, du.data_ptr(), None))
+        torch.cuda.synchronize()
+        qx = dq.cpu().numpy()
+        u = du.cpu().numpy().view(np.uint32)
+        for i in range(nb):
+            ref = orc.fwd_xform(q[i], dims)
+            assert np.array_equal(qx[i], ref)
+            assert np.array_equal(u[i], orc.fwd_reorder(ref, dims))
+        _ffi.check(L.gcow_stage_xform_device(dq.data_ptr(), nb, dims, 1, None))
+        torch.cuda.synchronize()
+        back = dq.cpu().numpy()
+        for i in range(nb):
+            assert np.array_equal(back[i], orc.inv_xform(qx[i], dims))
+
+
+# ---------------------------------------------------------------------------------------------- drop-in surface
+def _host_input(L, arr, dim):
+    """init_zfp_input over a malloc'd host copy (free_zfp_input frees it, as sw/ does)."""
+    libc = C.CDLL("libc.so.6")
+    libc.malloc.restype = C.c_void_p
+    libc.malloc.argtypes = [C.c_size_t]
+    buf = libc.malloc(arr.nbytes)
+    C.memmove(buf, arr.ctypes.data, arr.nbytes)
+    dims = [C.c_uint(s) for s in reversed(arr.shape)]
+    return L.init_zfp_input(C.c_void_p(buf), 3, C.c_uint(dim), *dims)
+
+
+def test_dropin_golden_flow(gc, orc):
+    """sw/tests/test_zfp.cpp:61-107 flow through the drop-in C ABI, host pointers."""
+    from gcow_amd import _ffi
+    L = _ffi.load()
+    for g in GOLDENS[:6]:
+        a = orc.gen_bump2d(g["n"], g["recipe"] == "bump_f32sum")
+        inp = _host_input(L, a, 2)
+        out = L.init_zfp_output(inp)
+        L.set_zfp_output_accuracy(out, 1e-3)
+        nbytes = L.zfp_compress(out, inp)
+        assert nbytes == g["bytes"]
+        b = C.string_at(out.contents.data.contents.begin, nbytes)
+        assert _sha(b) == g["sha256"]
+        # round trip through zfp_decompress (libzfp semantics)
+        L.stream_rewind(out.contents.data)
+        back = np.zeros_like(a)
+        inp2 = L.alloc_zfp_input()
+        inp2.contents.dtype = 3
+        inp2.contents.data = back.ctypes.data
+        inp2.contents.nx, inp2.contents.ny = g["n"], g["n"]
+        L.zfp_decompress(out, inp2)
+        ref = orc.decompress(np.frombuffer(b, np.uint64), a.shape, orc.accuracy(1e-3))
+        assert np.array_equal(back.view(np.uint32), ref.view(np.uint32))
+        inp2.contents.data = None
+        L.free_zfp_input(inp2)
+        L.cleanup(inp, out)
+
+
+def test_dropin_1d_3d_and_modes(gc, orc, fxa):
+    from gcow_amd import _ffi
+    L = _ffi.load()
+    for c in [c for c in FX if c["input"] in ("1d_n1000", "3d_9x10x7", "2d_special")]:
+        a = fxa["input__" + c["input"]]
+        inp = _host_input(L, a, a.ndim)
+        out = L.init_zfp_output(inp)
+        assert L.set_zfp_output_expert(out, *c["params"]) == 1
+        nbytes = L.zfp_compress(out, inp)
+        b = C.string_at(out.contents.data.contents.begin, nbytes)
+        assert _sha(b) == c["stream_sha256"], c["name"]
+        L.stream_rewind(out.contents.data)
+        back = np.zeros_like(a)
+        inp2 = L.alloc_zfp_input()
+        inp2.contents.dtype = 3
+        inp2.contents.data = back.ctypes.data
+        for i, s in enumerate(reversed(a.shape)):
+            setattr(inp2.contents, ["nx", "ny", "nz"][i], s)
+        L.zfp_decompress(out, inp2)
+        assert _sha(back.tobytes()) == c["decoded_sha256"], c["name"]
+        inp2.contents.data = None
+        L.free_zfp_input(inp2)
+        L.cleanup(inp, out)
+
+
+def test_block_api_known_answers(gc, orc):
+    """sw/tests/test_stages.cpp ENCODE_IBLOCK / ENCODE_ALL_BITPLANES / CAST through the drop-in block API."""
+    from gcow_amd import _ffi
+    L = _ffi.load()
+    KA = json.load(open(os.path.join(GOLD, "reference_known_answers.json")))
+    buf = (C.c_uint64 * 64)()
+    s = L.stream_init(C.cast(buf, C.c_void_p), C.sizeof(buf))
+    k = KA["encode_iblock"]
+    L.stream_write_bits(s, 2 * k["e"] + 1, 9)
+    ib = (C.c_int32 * 16)(*k["iblock"])
+    bits = L.encode_iblock(s, 1, 16658, k["expected_maxprec"], ib, 2)
+    assert bits == k["expected_iblock_bits"]
+    L.stream_flush(s)
+    assert [buf[0], buf[1]] == [int(x) for x in k["expected_words"]]
+    k = KA["encode_all_bitplanes"]
+    L.stream_rewind(s)
+    ub = (C.c_uint32 * 16)(*k["ublock"])
+    for _ in range(k["repeat"]):
+        L.stream_write_bits(s, 2 * (k["emax"] + 127) + 1, 9)
+        L.encode_all_bitplanes(s, ub, k["expected_maxprec"], 16)
+    L.stream_flush(s)
+    assert [buf[i] for i in range(9)] == [int(x) for x in k["expected_words"]]
+    k = KA["cast"]
+    bump = orc.gen_bump2d(3)
+    fb = (C.c_float * 16)()
+    L.gather_partial_2d_block(fb, bump.ctypes.data_as(C.POINTER(C.c_float)), 3, 3, 1, 3)
+    assert L.get_block_exponent(fb, 16) == 1
+    q = (C.c_int32 * 16)()
+    L.fwd_cast_block(q, fb, 16, 1)
+    assert list(q) == k["expected"]
+    L.fwd_decorrelate_2d_block(q)
+    assert list(q) == KA["decorrelate"]["expected"]
+    u = (C.c_uint32 * 16)()
+    perm = (C.c_ubyte * 16).in_dll(L, "PERM_2D")
+    L.fwd_reorder_int2uint(u, q, perm, 16)
+    assert list(u) == KA["reorder"]["expected"]
+
+
+def test_encode_fblock_decode_fblock(gc, orc):
+    from gcow_amd import _ffi
+    L = _ffi.load()
+    a = orc.gen_bump2d(8)
+    op = orc.accuracy(1e-3)
+    out = L.alloc_zfp_output()
+    L.set_zfp_output_accuracy(out, 1e-3)
+    buf = (C.c_uint64 * 256)()
+    out.contents.data = L.stream_init(C.cast(buf, C.c_void_p), C.sizeof(buf))
+    fb = (C.c_float * 16)()
+    for by in range(2):
+        for bx in range(2):
+            src = C.cast(C.c_void_p(a.ctypes.data + (4 * by * 8 + 4 * bx) * 4), C.POINTER(C.c_float))
+            L.gather_2d_block(fb, src, 1, 8)
+            L.encode_fblock(out, fb, 2)
+    L.stream_flush(out.contents.data)
+    nbytes = L.stream_size_bytes(out.contents.data)
+    w_ref, _ = orc.compress(a, op)
+    assert bytes(buf)[:nbytes] == w_ref.tobytes()
+    L.stream_rewind(out.contents.data)
+    ref = orc.decompress(w_ref, a.shape, op)
+    for by in range(2):
+        for bx in range(2):
+            L.decode_fblock(out, fb, 2)
+            blk = np.frombuffer(bytes(fb), np.float32).reshape(4, 4)
+            assert np.array_equal(blk.view(np.uint32), ref[4 * by:4 * by + 4, 4 * bx:4 * bx + 4].view(np.uint32))
+
+
+# ---------------------------------------------------------------------------------------------- full-size configs
+def test_c2_full_size_fixed_rate(gc, orc):
+    """BASELINE config 2: 256 Mi contiguous fp32, 1-D fixed rate 16 and 8, bit-exact vs the threaded oracle."""
+    n = 256 * 1024 * 1024
+    a = orc.gen_normal(n, 1e-3, 0x67636F77, True)
+    x = torch.from_numpy(a).cuda()
+    for r in (16, 8):
+        op = orc.rate(r, 1)
+        w_ref, bits_ref = orc.compress(a, op, threads=min(16, os.cpu_count() or 1))
+        e = gc.encode(x, P(gc, op))
+        torch.cuda.synchronize()
+        assert e.bits == bits_ref
+        got = e.stream().cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, w_ref)
+        del w_ref, got
+    # round-trip property at full size: decode(encode(x)) for rate 16 equals the oracle decode of a slice
+    e = gc.encode(x, P(gc, orc.rate(16, 1)))
+    d = gc.decode(e)
+    torch.cuda.synchronize()
+    lo = 12345 * 4
+    w_ref, _ = orc.compress(a[lo:lo + 4096], orc.rate(16, 1))
+    ref = orc.decompress(w_ref, (4096,), orc.rate(16, 1))
+    assert np.array_equal(d[lo:lo + 4096].cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def test_c3_full_size_roundtrip(gc, orc):
+    """BASELINE config 3: 512^3 fp32 volume, 3-D fixed rate 8 and accuracy 1e-3, encode + decode vs the oracle."""
+    n = 512
+    x = np.arange(n, dtype=np.float64) / n
+    g = (np.sin(6 * np.pi * x)[None, None, :].astype(np.float32) *
+         np.cos(4 * np.pi * x)[None, :, None].astype(np.float32) *
+         np.sin(2 * np.pi * x)[:, None, None].astype(np.float32))
+    g += 1e-3 * orc.gen_normal(n ** 3, 1.0, 21, False).reshape(n, n, n)
+    a = np.ascontiguousarray(g, dtype=np.float32)
+    del g
+    xt = torch.from_numpy(a).cuda()
+    for op, stride in ((orc.rate(8, 3), 0), (orc.accuracy(1e-3), 1)):
+        w_ref, bits_ref = orc.compress(a, op, threads=min(16, os.cpu_count() or 1))
+        e = gc.encode(xt, P(gc, op), index_stride=stride)
+        torch.cuda.synchronize()
+        assert e.bits == bits_ref
+        assert np.array_equal(e.stream().cpu().numpy().view(np.uint64), w_ref)
+        d = gc.decode(e).cpu().numpy()
+        # decoded values bit-identical to the oracle (libzfp semantics) on a slab, and within tolerance everywhere
+        sl = (slice(100, 108), slice(0, 512), slice(0, 512))
+        w_sl, _ = orc.compress(np.ascontiguousarray(a[sl]), op)
+        ref = orc.decompress(w_sl, a[sl].shape, op)
+        assert np.array_equal(d[sl].view(np.uint32), ref.view(np.uint32))
+        if op.minbits != op.maxbits:
+            assert float(np.max(np.abs(d - a))) <= 1e-3
+        del w_ref, d
