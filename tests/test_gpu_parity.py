@@ -412,3 +412,19 @@ def test_c3_full_size_roundtrip(gc, orc):
         if op.minbits != op.maxbits:
             assert float(np.max(np.abs(d - a))) <= 1e-3
         del w_ref, d
+
+
+@pytest.mark.parametrize("r", [16, 8])
+def test_fast1d_adversarial_blocks(gc, orc, r):
+    """Blocks whose coefficients differ by many binades (long group-test phases beyond one 16-plane window),
+    constant / alternating blocks (zero high-frequency coefficients), powers of two, mixed signs."""
+    rng = np.random.default_rng(17)
+    nb = 1 << 16
+    sign = np.where(rng.random((nb, 4)) < 0.5, -1.0, 1.0)
+    wide = sign * 2.0 ** rng.uniform(-40, 0, (nb, 4))
+    const = np.repeat(rng.standard_normal((nb // 4, 1)), 4, axis=1)
+    alt = np.repeat(rng.standard_normal((nb // 4, 1)), 4, axis=1) * np.array([1, -1, 1, -1])
+    pow2 = 2.0 ** rng.integers(-30, 30, (nb // 4, 4)) * np.where(rng.random((nb // 4, 4)) < 0.5, -1.0, 1.0)
+    ramp = np.cumsum(rng.standard_normal((nb // 4, 4)) * 1e-6, axis=1) + 1.0
+    a = np.concatenate([wide, const, alt, pow2, ramp]).astype(np.float32).reshape(-1)
+    _check_vs_oracle(gc, orc, a, orc.rate(r, 1))

@@ -1,0 +1,35 @@
+"""Interleaved A/B timing of the ablation kernels (one process, rounds interleaved; cdna guide 5.4 rule 24)."""
+import ctypes as C
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+from gcow_amd import codec  # noqa: E402
+
+L = C.CDLL(os.path.join(HERE, "libablate.so"))
+L.ablate_run.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p]
+n = 256 * 1024 * 1024
+x = torch.empty(n, dtype=torch.float32, device="cuda")
+codec.fill_normal(x)
+out = torch.empty(n // 4, dtype=torch.int64, device="cuda")
+st = torch.cuda.current_stream()
+modes = [int(m) for m in (sys.argv[1].split(",") if len(sys.argv) > 1 else "0,1,2,3,4".split(","))]
+wgs = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+res = {m: [] for m in modes}
+for rnd in range(6):
+    for m in modes:
+        for _ in range(2):
+            L.ablate_run(m, x.data_ptr(), n // 4, out.data_ptr(), wgs, st.cuda_stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(10):
+            L.ablate_run(m, x.data_ptr(), n // 4, out.data_ptr(), wgs, st.cuda_stream)
+        e1.record(st)
+        torch.cuda.synchronize()
+        res[m].append(e0.elapsed_time(e1) / 10)
+for m in modes:
+    v = sorted(res[m])
+    print("mode %d wgs %d: median %.4f ms  min %.4f ms  (%.0f GB/s algorithmic)" % (m, wgs, v[len(v) // 2], v[0], 1.5 * 2**30 / (v[len(v)//2] / 1e3) / 1e9))
