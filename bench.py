@@ -151,25 +151,37 @@ def main():
     # RCCL all-gather of the compressed shards (C4 exchange step), timed on its own
     if world > 1 and not args.no_allgather:
         from gcow_amd import dist as gdist
+        nb = n // 4
         e = enc(x, stream)
         for _ in range(2):
-            gdist.allgather_fixed(e)
+            full = gdist.allgather_fixed(e.words, nb, p.maxbits)
         torch.cuda.synchronize()
         dist.barrier()
         ta = time.perf_counter()
         reps = max(3, args.steps // 4)
         for _ in range(reps):
             e = enc(x, stream)
-            full = gdist.allgather_fixed(e)
+            full = gdist.allgather_fixed(e.words, nb, p.maxbits)
         torch.cuda.synchronize()
         dist.barrier()
         ag_ms = (time.perf_counter() - ta) * 1e3 / reps
         t = torch.tensor([ag_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ag_ms = t.item()
+        # parity of the gathered single stream: rank 0 re-encodes every rank's shard locally and compares
+        ok = True
+        if rank == 0:
+            y = torch.empty_like(x)
+            shard_words = nb * p.maxbits // 64
+            for r in range(world):
+                codec.fill_normal(y, 1e-3, seed=0x67636F77 + r, inject=True)
+                er = codec.encode(y, p)
+                ok = ok and bool(torch.equal(er.words[:shard_words], full[r * shard_words:(r + 1) * shard_words]))
+            del y
         extra["encode_allgather"] = {"ms_per_step": round(ag_ms, 4),
                                      "GiBps_input": round(world * in_bytes / (ag_ms / 1e3) / 2 ** 30, 2),
-                                     "gathered_bytes_per_rank": int(full.numel() * 8)}
+                                     "gathered_bytes_per_rank": int(full.numel() * 8),
+                                     "gathered_stream_equals_single_gpu_encode": ok}
         del full
 
     if rank == 0 and world == 1 and not args.no_host_e2e:
@@ -201,7 +213,7 @@ def main():
             cpu = {"error": repr(ex)}
 
     if rank == 0:
-        kname = "k_encode_fixed1d"
+        kname = "k_encode_fixed1d_pnt"
         traffic = load_pmc_traffic(kname, workload)
         line = {
             "metric": "GiB/s device-resident fp32->ZFP encode, 256Mi-float bucket, 1/2/4/8 GPU",

@@ -5,21 +5,26 @@ The reference never puts compressed bytes on a wire (its DDP all-reduce runs on 
 hw/models/train_imagenet.py:446-475); this is the exchange step north_star asks for.
 
 Fixed rate: every block is maxbits long, so shard r's stream occupies bits [r*S*maxbits, ...) of the full stream;
-with S*maxbits a multiple of 64 one all_gather_into_tensor of equal-size shard streams IS the single-GPU stream.
-Variable rate: all-gather the per-rank bit lengths, all-gather streams padded to the longest, then bit-stitch each
-shard at its exclusive-prefix bit offset on the device (gcow_stitch_device).
+with S*maxbits a multiple of 64 one all-gather of equal-size shard streams IS the single-GPU stream (byte-identical
+to encoding the whole bucket on one GPU).
+Variable rate: all-gather the per-rank bit lengths, all-gather the streams padded to the longest, then bit-stitch
+shard r at its exclusive-prefix bit offset (gcow_stitch_device on the GPU). Per-shard flush padding is dropped:
+offsets use the unflushed bit counts.
+
+The protocol functions take plain int64 word tensors, so the same code runs over RCCL on device tensors and over
+gloo on CPU tensors (tests/test_dist_cpu.py).
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
-from . import codec
 from ._ffi import GcowError
 
 
-def shard_bounds(nvals: int, world: int, rank: int, block: int = 4, align_blocks: int = 1):
-    """Contiguous block-aligned shard [lo, hi) of a 1-D bucket of nvals values for `rank`."""
+def shard_bounds(nvals: int, world: int, rank: int, block: int = 4, align_blocks: int = 16):
+    """Contiguous block-aligned shard [lo, hi) of a 1-D bucket of nvals values for `rank`. align_blocks = 16 makes
+    every full shard end on a 64-bit stream boundary at any rate with 4 * rate integral."""
     nblocks = (nvals + block - 1) // block
     per = (nblocks + world - 1) // world
     per = (per + align_blocks - 1) // align_blocks * align_blocks
@@ -28,49 +33,65 @@ def shard_bounds(nvals: int, world: int, rank: int, block: int = 4, align_blocks
     return min(lo_b * block, nvals), min(hi_b * block, nvals)
 
 
-def allgather_fixed(enc: codec.Encoded, group=None) -> torch.Tensor:
-    """All-gather equal-size fixed-rate shard streams: the result is the single-stream sw/ layout."""
-    p = enc.params
-    nblocks = 1
-    for s in enc.shape:
-        nblocks *= (s + 3) // 4
-    if (nblocks * p.maxbits) % 64:
+def _allgather_into(out: torch.Tensor, local: torch.Tensor, group=None):
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, local, group=group)
+    else:
+        world = dist.get_world_size(group)
+        dist.all_gather(list(out.chunk(world)), local, group=group)
+
+
+def allgather_fixed(words: torch.Tensor, nblocks: int, maxbits: int, group=None) -> torch.Tensor:
+    """All-gather equal-size fixed-rate shard streams (each shard nblocks blocks of maxbits bits)."""
+    if (nblocks * maxbits) % 64:
         raise GcowError("fixed-rate shard must end on a 64-bit boundary (shard blocks * maxbits % 64 == 0)")
-    words = nblocks * p.maxbits // 64
-    local = enc.words[:words]
+    nw = nblocks * maxbits // 64
+    local = words[:nw].contiguous()
     world = dist.get_world_size(group)
-    out = torch.empty(world * words, dtype=torch.int64, device=local.device)
-    dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    out = torch.empty(world * nw, dtype=torch.int64, device=local.device)
+    _allgather_into(out, local, group)
     return out
 
 
-def allgather_variable(enc: codec.Encoded, group=None):
-    """All-gather variable-rate shard streams and stitch them into one stream. Returns (words, total_bits)."""
+def allgather_variable(words: torch.Tensor, bits: int, group=None, stitch=None):
+    """All-gather variable-rate shard streams and stitch them into one stream. Returns (words, total_bits).
+    `stitch(dst, dst_bit_offset, src, src_bits)` defaults to the device kernel (gcow_stitch_device)."""
+    if stitch is None:
+        from .codec import stitch as _dev_stitch
+        stitch = _dev_stitch
     world = dist.get_world_size(group)
-    bits_local = enc.bits_dev.reshape(1)
-    lens = torch.empty(world, dtype=torch.int64, device=bits_local.device)
-    dist.all_gather_into_tensor(lens, bits_local, group=group)
-    lens_h = lens.cpu().tolist()
-    maxw = max((b + 63) // 64 for b in lens_h) if lens_h else 0
-    maxw = max(maxw, 1)
-    local = torch.zeros(maxw, dtype=torch.int64, device=bits_local.device)
-    nw = (lens_h[dist.get_rank(group)] + 63) // 64
-    local[:nw] = enc.words[:nw]
-    gathered = torch.empty(world * maxw, dtype=torch.int64, device=local.device)
-    dist.all_gather_into_tensor(gathered, local, group=group)
+    dev = words.device
+    lens = torch.zeros(world, dtype=torch.int64, device=dev)
+    mine = torch.tensor([int(bits)], dtype=torch.int64, device=dev)
+    _allgather_into(lens, mine, group)
+    lens_h = [int(v) for v in lens.cpu().tolist()]
+    maxw = max(1, max((b + 63) // 64 for b in lens_h))
+    local = torch.zeros(maxw, dtype=torch.int64, device=dev)
+    nw = (int(bits) + 63) // 64
+    local[:nw] = words[:nw]
+    gathered = torch.empty(world * maxw, dtype=torch.int64, device=dev)
+    _allgather_into(gathered, local, group)
     total = sum(lens_h)
-    out = torch.zeros((total + 63) // 64 + 1, dtype=torch.int64, device=local.device)
+    out = torch.zeros((total + 63) // 64 + 1, dtype=torch.int64, device=dev)
     off = 0
     for r in range(world):
-        codec.stitch(out, off, gathered[r * maxw:(r + 1) * maxw], lens_h[r])
+        if lens_h[r]:
+            stitch(out, off, gathered[r * maxw:(r + 1) * maxw], lens_h[r])
         off += lens_h[r]
     return out[: (total + 63) // 64], total
 
 
-def encode_allgather(bucket_shard: torch.Tensor, params, group=None):
-    """Encode this rank's 1-D shard and rebuild the full stream on every rank. Returns (words, total_bits)."""
-    enc = codec.encode(bucket_shard, params)
-    if codec.is_fixed(params):
-        words = allgather_fixed(enc, group)
-        return words, words.numel() * 64
-    return allgather_variable(enc, group)
+def encode_allgather(bucket: torch.Tensor, params, group=None):
+    """Encode this rank's contiguous shard of a 1-D bucket (replicated on every rank: the C4 layout) and rebuild the
+    full stream on every rank. Returns (words, total_bits)."""
+    from . import codec
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    bounds = [shard_bounds(bucket.numel(), world, r) for r in range(world)]
+    lo, hi = bounds[rank]
+    enc = codec.encode(bucket[lo:hi], params)
+    sizes = {b - a for a, b in bounds}
+    nb = (hi - lo + 3) // 4
+    if codec.is_fixed(params) and len(sizes) == 1 and (hi - lo) % 4 == 0 and (nb * params.maxbits) % 64 == 0:
+        words = allgather_fixed(enc.words, nb, params.maxbits, group)
+        return words, world * nb * params.maxbits
+    return allgather_variable(enc.words, enc.bits, group)

@@ -1,0 +1,132 @@
+#!/usr/bin/env python3
+"""Secondary measurements for BASELINE configs 3 and 5 and the decoder (one JSON line per case, 1 GPU).
+
+  c2_decode   256 Mi fp32 1-D rate 16: decode throughput
+  c2_rate8    256 Mi fp32 1-D rate 8 encode
+  c3          512^3 fp32 3-D: encode + decode, fixed rate 8 and accuracy 1e-3 (with block index)
+  c5          256 Mi bf16 1-D variable rate (accuracy 1e-6 / 1e-3): device encode, and the host-resident
+              path (pinned H2D of the bf16 bucket + encode + D2H of the stream)
+  var_f32     256 Mi fp32 1-D accuracy 1e-6 / 1e-3 encode
+Timing: HIP events on the launching stream, median of interleaved rounds.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from gcow_amd import codec  # noqa: E402
+
+
+def timeit(fn, reps=10, rounds=3):
+    st = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / reps)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def c2_decode():
+    n = 256 << 20
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    codec.fill_normal(x)
+    p = codec.rate(16, 1)
+    e = codec.encode(x, p)
+    out = torch.empty_like(x)
+    ms = timeit(lambda: codec.decode(e, out=out))
+    emit(case="c2_decode_rate16", ms=round(ms, 4), GiBps_output=round(n * 4 / (ms / 1e3) / 2 ** 30, 1),
+         GBps_traffic=round((n * 4 + n * 2) / (ms / 1e3) / 1e9, 1))
+    p8 = codec.rate(8, 1)
+    enc8 = codec.Encoder((n,), torch.float32, p8)
+    ms = timeit(lambda: enc8(x))
+    emit(case="c2_encode_rate8", ms=round(ms, 4), GiBps_input=round(n * 4 / (ms / 1e3) / 2 ** 30, 1))
+
+
+def c3():
+    n = 512
+    g = torch.arange(n, device="cuda", dtype=torch.float64) / n
+    x = (torch.sin(6 * math.pi * g)[None, None, :] * torch.cos(4 * math.pi * g)[None, :, None] *
+         torch.sin(2 * math.pi * g)[:, None, None]).float()
+    noise = torch.empty(n ** 3, dtype=torch.float32, device="cuda")
+    codec.fill_normal(noise, 1e-3, inject=False)
+    x += noise.view(n, n, n)
+    del noise
+    for name, p, stride in (("rate8", codec.rate(8, 3), 0), ("acc1e-3", codec.accuracy(1e-3), 1)):
+        enc = codec.Encoder(x.shape, torch.float32, p, index_stride=stride)
+        ms_e = timeit(lambda: enc(x), reps=5)
+        e = enc(x)
+        bits = e.bits
+        out = torch.empty_like(x)
+        ms_d = timeit(lambda: codec.decode(e, out=out), reps=5)
+        err = float((out - x).abs().max())
+        emit(case="c3_%s" % name, encode_ms=round(ms_e, 3), decode_ms=round(ms_d, 3),
+             encode_GiBps=round(x.numel() * 4 / (ms_e / 1e3) / 2 ** 30, 1),
+             decode_GiBps=round(x.numel() * 4 / (ms_d / 1e3) / 2 ** 30, 1),
+             roundtrip_GiBps=round(x.numel() * 4 / ((ms_e + ms_d) / 1e3) / 2 ** 30, 1),
+             bits_per_value=round(bits / x.numel(), 3), max_abs_err=err)
+
+
+def var_f32():
+    n = 256 << 20
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    codec.fill_normal(x)
+    for tol in (1e-6, 1e-3):
+        enc = codec.Encoder((n,), torch.float32, codec.accuracy(tol))
+        ms = timeit(lambda: enc(x), reps=5)
+        e = enc(x)
+        emit(case="var_f32_acc%g" % tol, ms=round(ms, 3), GiBps_input=round(n * 4 / (ms / 1e3) / 2 ** 30, 1),
+             bits_per_value=round(e.bits / n, 3))
+
+
+def c5():
+    n = 256 << 20
+    xf = torch.empty(n, dtype=torch.float32, device="cuda")
+    codec.fill_normal(xf)
+    xb = xf.to(torch.bfloat16)
+    del xf
+    for tol in (1e-6, 1e-3):
+        p = codec.accuracy(tol)
+        enc = codec.Encoder((n,), torch.bfloat16, p)
+        ms = timeit(lambda: enc(xb), reps=5)
+        e = enc(xb)
+        bits = e.bits
+        nw = (bits + 63) // 64
+        h_in = xb.cpu().pin_memory()
+        h_out = torch.empty(nw, dtype=torch.int64, pin_memory=True)
+        d_in = torch.empty_like(xb)
+
+        def host_path():
+            d_in.copy_(h_in, non_blocking=True)
+            ee = enc(d_in)
+            h_out.copy_(ee.words[:nw], non_blocking=True)
+
+        ms_h = timeit(host_path, reps=3)
+        emit(case="c5_bf16_acc%g" % tol, encode_ms=round(ms, 3),
+             encode_GiBps_input=round(n * 2 / (ms / 1e3) / 2 ** 30, 1), bits_per_value=round(bits / n, 3),
+             host_path_ms=round(ms_h, 3), host_path_GiBps_input=round(n * 2 / (ms_h / 1e3) / 2 ** 30, 2))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cases", nargs="*", default=["c2_decode", "c3", "var_f32", "c5"])
+    a = ap.parse_args()
+    for c in a.cases:
+        globals()[c]()
