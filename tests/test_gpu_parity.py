@@ -428,3 +428,45 @@ def test_fast1d_adversarial_blocks(gc, orc, r):
     ramp = np.cumsum(rng.standard_normal((nb // 4, 4)) * 1e-6, axis=1) + 1.0
     a = np.concatenate([wide, const, alt, pow2, ramp]).astype(np.float32).reshape(-1)
     _check_vs_oracle(gc, orc, a, orc.rate(r, 1))
+
+
+# ---------------------------------------------------------------------------------------------- DDP hooks
+def _ddp_single_rank(hook_name, params):
+    import torch.distributed as dist
+    from gcow_amd import ddp
+    if not dist.is_initialized():
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(64, 96), torch.nn.ReLU(), torch.nn.Linear(96, 10)).cuda()
+    ref_model = torch.nn.Sequential(torch.nn.Linear(64, 96), torch.nn.ReLU(), torch.nn.Linear(96, 10)).cuda()
+    ref_model.load_state_dict(model.state_dict())
+    dm = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=1)
+    state = ddp.GcowHookState(params=params)
+    dm.register_comm_hook(state, getattr(ddp, hook_name))
+    x = torch.randn(32, 64, device="cuda")
+    dm(x).square().mean().backward()
+    ref_model(x).square().mean().backward()
+    return model, ref_model
+
+
+@pytest.mark.parametrize("hook", ["roundtrip_hook", "compressed_allgather_hook"])
+@pytest.mark.parametrize("mode", ["rate16", "acc1e-6"])
+def test_ddp_hooks_single_rank(gc, orc, hook, mode):
+    """With one rank both hooks leave every gradient equal to decode(encode(grad)) of its flattened bucket; the
+    per-element error is within the codec's bound."""
+    params = gc.rate(16, 1) if mode == "rate16" else gc.accuracy(1e-6)
+    model, ref_model = _ddp_single_rank(hook, params)
+    for p, q in zip(model.parameters(), ref_model.parameters()):
+        assert p.grad is not None
+        err = (p.grad - q.grad).abs().max().item()
+        scale = q.grad.abs().max().item()
+        if mode == "acc1e-6":
+            assert err <= 1e-6
+        else:
+            assert err <= 2.0 ** -10 * max(scale, 1e-30)  # 16 bits/value on smooth-ish gradients
