@@ -216,3 +216,74 @@ def fill_normal(out: torch.Tensor, sigma: float = 1e-3, seed: int = 0x67636F77, 
     check(load().gcow_fill_normal_device(out.data_ptr(), out.numel(), sigma, seed, int(inject),
                                          _stream_ptr(stream)), "gcow_fill_normal_device")
     return out
+
+
+# ------------------------------------------------------------------------------------------- zfpy byte streams
+def write_header(shape, params: GcowParams, dtype=torch.float32):
+    """(header words [3 x uint64 as python ints], header bits) of zfp_write_header(ZFP_HEADER_FULL)."""
+    f = field_of_shape(shape, dtype)
+    w = (C.c_uint64 * 3)()
+    bits = load().gcow_write_header(C.byref(f), C.byref(params), w)
+    if not bits:
+        raise GcowError("shape %s has no zfp header form" % (tuple(shape),))
+    return [int(x) for x in w], int(bits)
+
+
+def read_header(words):
+    """Parse a zfp 0.5.5 header from the first words (host ints, numpy or a tensor) -> (shape, params, bits)."""
+    if isinstance(words, torch.Tensor):
+        words = words[:3].cpu().tolist()
+    w = [int(x) & 0xFFFFFFFFFFFFFFFF for x in list(words)[:3]]
+    w += [0] * (3 - len(w))
+    arr = (C.c_uint64 * 3)(*w)
+    f, p = ZfpInput(), GcowParams()
+    bits = load().gcow_read_header(arr, 3, C.byref(f), C.byref(p))
+    if not bits:
+        raise GcowError("not a zfp 0.5.5 float stream (bad magic, version or type)")
+    shape = tuple(n for n in (f.nz, f.ny, f.nx) if n)
+    return shape, p, int(bits)
+
+
+def compress_numpy(x: torch.Tensor, tolerance: float = -1, rate: float = -1, precision: int = -1,
+                   stream=None) -> torch.Tensor:
+    """zfpy.compress_numpy for a device tensor: header + stream, byte-identical to zfpy/libzfp 0.5.5 (returned as an
+    int64 device tensor of ceil(bits/64) words). Same keyword semantics as zfpy: exactly one of tolerance / rate /
+    precision >= 0 selects the mode."""
+    if tolerance >= 0:
+        p = accuracy(tolerance)
+    elif rate >= 0:
+        p = globals()["rate"](rate, x.dim())
+    elif precision >= 0:
+        p = globals()["precision"](precision)
+    else:
+        p = expert(ZFP_MIN_BITS, ZFP_MAX_BITS - 1, ZFP_MAX_PREC, ZFP_MIN_EXP)  # zfpy default: lossless-ish expert
+    return compress_zfp(x, p, stream)
+
+
+def compress_zfp(x: torch.Tensor, params: GcowParams, stream=None) -> torch.Tensor:
+    if not x.is_cuda:
+        raise GcowError("compress_zfp expects a device tensor")
+    L = load()
+    f = field_of(x)
+    cap = L.gcow_max_output_bytes(C.byref(f), C.byref(params)) + 24
+    ws_bytes = L.gcow_encode_zfp_workspace_bytes(C.byref(f), C.byref(params))
+    out = torch.zeros((cap + 7) // 8, dtype=torch.int64, device=x.device)
+    ws = torch.zeros((ws_bytes + 7) // 8, dtype=torch.int64, device=x.device)
+    bits = torch.zeros(1, dtype=torch.int64, device=x.device)
+    check(L.gcow_encode_device_zfp(C.byref(f), C.byref(params), out.data_ptr(), cap, bits.data_ptr(), ws.data_ptr(),
+                                   ws_bytes, _stream_ptr(stream)), "gcow_encode_device_zfp")
+    return out[: (int(bits.item()) + 63) // 64]
+
+
+def decompress_numpy(words: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """zfpy.decompress_numpy for a device stream with a zfp header: shape and mode come from the header."""
+    shape, p, hb = read_header(words)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=words.device)
+    elif tuple(out.shape) != shape:
+        raise GcowError("output shape %s does not match the header's %s" % (tuple(out.shape), shape))
+    w = torch.cat([words.reshape(-1), torch.zeros(2, dtype=torch.int64, device=words.device)])
+    f = field_of(out)
+    check(load().gcow_decode_device_at(C.byref(f), C.byref(p), w.data_ptr(), w.numel() * 8, hb, None, 0,
+                                       _stream_ptr(stream)), "gcow_decode_device_at")
+    return out

@@ -700,6 +700,160 @@ gcow_status gcow_decode_device(const zfp_input* field, const gcow_params* p, con
   return decode_impl(field, p, d_in, d_index, index_stride, 0, nullptr, hip_stream);
 }
 
+// ---------------------------------------------------------------------------------------------- zfp header
+// Restates libzfp 0.5.5 zfp_field_metadata / zfp_stream_mode / zfp_write_header / zfp_read_header / zfp_stream_set_mode
+// (third-party format; pinned by tests/golden/libzfp_headers.json).
+static const uint32_t kMinBits = 1, kMaxBits = 16657, kMaxPrec = 64;
+static const int32_t kMinExp = -1074;
+
+static uint64_t hdr_mode(const gcow_params& p)
+{
+  const bool valid = p.minbits <= p.maxbits && p.maxprec >= 1 && p.maxprec <= 64;
+  const bool dflt = p.minbits == kMinBits && p.maxbits == kMaxBits && p.maxprec == kMaxPrec && p.minexp == kMinExp;
+  if (valid && !dflt) {
+    if (p.minbits == p.maxbits && p.maxbits >= 1 && p.maxbits <= kMaxBits && p.maxprec >= kMaxPrec &&
+        p.minexp <= kMinExp) {
+      if (p.maxbits <= 2048) return p.maxbits - 1;
+    } else if (p.minbits <= kMinBits && p.maxbits >= kMaxBits && p.minexp <= kMinExp) {
+      if (p.maxprec <= 128) return (uint64_t)(p.maxprec - 1) + 2048;
+    } else if (p.minbits <= kMinBits && p.maxbits >= kMaxBits && p.maxprec >= kMaxPrec && p.minexp >= kMinExp) {
+      if (p.minexp <= 843) return (uint64_t)(p.minexp - kMinExp) + 2177;
+    }
+  }
+  uint64_t m = (uint64_t)std::max(0, std::min(p.minexp + 16495, 0x7fff));
+  m = (m << 7) + (std::max(1u, std::min(p.maxprec, 0x80u)) - 1);
+  m = (m << 15) + (std::max(1u, std::min(p.maxbits, 0x8000u)) - 1);
+  m = (m << 15) + (std::max(1u, std::min(p.minbits, 0x8000u)) - 1);
+  return (m << 12) + 0xfffu;
+}
+
+static void put_bits(uint64_t* w, uint32_t& pos, uint64_t v, uint32_t n)
+{
+  if (n < 64) v &= (1ull << n) - 1ull;
+  const uint32_t sh = pos & 63;
+  w[pos >> 6] |= v << sh;
+  if (sh && sh + n > 64) w[(pos >> 6) + 1] |= v >> (64 - sh);
+  pos += n;
+}
+
+static uint64_t get_bits(const uint64_t* w, uint32_t& pos, uint32_t n)
+{
+  const uint32_t sh = pos & 63;
+  uint64_t v = w[pos >> 6] >> sh;
+  if (sh && sh + n > 64) v |= w[(pos >> 6) + 1] << (64 - sh);
+  if (n < 64) v &= (1ull << n) - 1ull;
+  pos += n;
+  return v;
+}
+
+uint gcow_header_bits(const gcow_params* p) { return p && hdr_mode(*p) < 0xfffu ? 96u : 148u; }
+
+uint gcow_write_header(const zfp_input* field, const gcow_params* p, uint64_t* words)
+{
+  const uint32_t d = dims_of(field);
+  if (!p || !words || d < 1 || d > 3) return 0;
+  const size_t n[3] = {field->nx, field->ny, field->nz};
+  const uint32_t w = d == 1 ? 48 : d == 2 ? 24 : 16;
+  for (uint32_t a = 0; a < d; a++)
+    if (n[a] == 0 || (w < 64 && (uint64_t)(n[a] - 1) >> w)) return 0;
+  uint64_t meta = 0;
+  for (int a = (int)d - 1; a >= 0; a--) meta = (meta << w) + (uint64_t)(n[a] - 1);
+  meta = (meta << 2) + (d - 1);
+  meta = (meta << 2) + 2;  // zfp_type_float - 1
+  words[0] = words[1] = words[2] = 0;
+  uint32_t pos = 0;
+  put_bits(words, pos, 0x0570667aull, 32);  // 'z' 'f' 'p' version 5
+  put_bits(words, pos, meta, 52);
+  const uint64_t mode = hdr_mode(*p);
+  put_bits(words, pos, mode, mode < 0xfffu ? 12 : 64);
+  return pos;
+}
+
+uint gcow_read_header(const uint64_t* words, size_t nwords, zfp_input* field, gcow_params* p)
+{
+  if (!words || !field || !p || nwords < 2) return 0;
+  uint64_t w[3] = {words[0], words[1], nwords > 2 ? words[2] : 0};
+  uint32_t pos = 0;
+  if (get_bits(w, pos, 32) != 0x0570667aull) return 0;
+  uint64_t meta = get_bits(w, pos, 52);
+  if ((meta & 3u) + 1 != 3) return 0;  // float only
+  meta >>= 2;
+  const uint32_t d = (uint32_t)(meta & 3u) + 1;
+  meta >>= 2;
+  if (d > 3) return 0;
+  const uint32_t bw = d == 1 ? 48 : d == 2 ? 24 : 16;
+  size_t n[3] = {0, 0, 0};
+  for (uint32_t a = 0; a < d; a++) {
+    n[a] = (size_t)(meta & ((1ull << bw) - 1)) + 1;
+    meta >>= bw;
+  }
+  uint64_t mode = get_bits(w, pos, 12);
+  gcow_params q{};
+  if (mode < 0xfffu) {
+    if (mode < 2048) {
+      q = gcow_params{(uint)mode + 1, (uint)mode + 1, kMaxPrec, kMinExp};
+    } else if (mode < 2048 + 128) {
+      q = gcow_params{kMinBits, kMaxBits, (uint)mode + 1 - 2048, kMinExp};
+    } else {
+      q = gcow_params{kMinBits, kMaxBits, kMaxPrec, (int)mode + kMinExp - 2177};
+    }
+  } else {
+    if (nwords < 3) return 0;
+    mode = (mode + (get_bits(w, pos, 52) << 12)) >> 12;
+    q.minbits = (uint)(mode & 0x7fffu) + 1;
+    mode >>= 15;
+    q.maxbits = (uint)(mode & 0x7fffu) + 1;
+    mode >>= 15;
+    q.maxprec = (uint)(mode & 0x7fu) + 1;
+    mode >>= 7;
+    q.minexp = (int)(mode & 0x7fffu) - 16495;
+  }
+  field->dtype = dtype_float;
+  field->nx = n[0];
+  field->ny = n[1];
+  field->nz = n[2];
+  field->nw = 0;
+  *p = q;
+  return pos;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t gcow_encode_zfp_workspace_bytes(const zfp_input* field, const gcow_params* p)
+{
+  return align256(gcow_encode_workspace_bytes(field, p)) + 256 + align256(gcow_max_output_bytes(field, p));
+}
+
+gcow_status gcow_encode_device_zfp(const zfp_input* field, const gcow_params* p, void* d_out, size_t out_capacity,
+                                   uint64_t* d_total_bits, void* d_workspace, size_t workspace_bytes,
+                                   void* hip_stream)
+{
+  uint64_t h[3];
+  const uint32_t hb = gcow_write_header(field, p, h);
+  if (!hb) return fail(GCOW_ERR_INVALID, "field shape not representable in a zfp header (dims 1-3)");
+  const size_t bound = gcow_max_output_bytes(field, p);
+  if (!d_out || out_capacity < bound + 24) return fail(GCOW_ERR_CAPACITY, "output capacity below bound + 24");
+  if (!d_workspace || workspace_bytes < gcow_encode_zfp_workspace_bytes(field, p))
+    return fail(GCOW_ERR_INVALID, "workspace smaller than gcow_encode_zfp_workspace_bytes()");
+  const size_t ews = gcow_encode_workspace_bytes(field, p);
+  char* ws = (char*)d_workspace;
+  uint64_t* d_bits = (uint64_t*)(ws + align256(ews));
+  void* d_tmp = ws + align256(ews) + 256;
+  gcow_status st = encode_impl(field, p, d_tmp, bound, d_bits, ews ? ws : nullptr, ews, nullptr, 0, hip_stream);
+  if (st) return st;
+  GCOW_HIP(gcow::launch_prepend_header((uint64_t*)d_out, hb, (const uint64_t*)d_tmp, d_bits, h,
+                                       (uint64_t)(bound / 8) + 3, d_total_bits, hip_stream));
+  return GCOW_OK;
+}
+
+gcow_status gcow_decode_device_at(const zfp_input* field, const gcow_params* p, const void* d_in, size_t in_bytes,
+                                  uint64_t bit_offset, const uint64_t* d_index, uint32_t index_stride,
+                                  void* hip_stream)
+{
+  (void)in_bytes;
+  return decode_impl(field, p, d_in, d_index, index_stride, bit_offset, nullptr, hip_stream);
+}
+
 gcow_status gcow_stitch_device(uint64_t* d_dst, uint64_t dst_bit_offset, const uint64_t* d_src, uint64_t src_bits,
                                void* hip_stream)
 {

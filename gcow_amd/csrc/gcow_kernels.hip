@@ -1012,6 +1012,42 @@ __global__ __launch_bounds__(64) void k_decode(FieldDesc F, Params p, const uint
 
 __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 
+// ------------------------------------------------------------------------------------------------ header stream
+// dst = header bits [0, off) followed by src bits [0, *d_bits), flushed to whole words (zfp_write_header then
+// zfp_compress at the following bit). Plain stores, one lane per destination word; lanes past the end exit. Lane 0
+// also publishes the total bit count.
+__global__ void k_prepend_header(uint64_t* __restrict__ dst, uint32_t off, const uint64_t* __restrict__ src,
+                                 const uint64_t* __restrict__ d_bits, uint64_t h0, uint64_t h1, uint64_t h2,
+                                 uint64_t* __restrict__ d_total)
+{
+  const uint64_t bits = *d_bits, end = off + bits;
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w == 0 && d_total) *d_total = end;
+  if ((w << 6) >= end) return;
+  const uint64_t nsw = (bits + 63) >> 6;
+  uint64_t v = 0;
+  if (w < 3 && (w << 6) < off) {  // header part of this word
+    const uint64_t h = w == 0 ? h0 : (w == 1 ? h1 : h2);
+    const uint64_t hb = off - (w << 6);
+    v = hb >= 64 ? h : (h & ((1ull << hb) - 1ull));
+  }
+  const int64_t s = (int64_t)(w << 6) - (int64_t)off;  // source bit landing on bit 0 of dst[w]
+  if (s + 64 > 0 && nsw) {
+    if (s < 0) {
+      v |= src[0] << (uint32_t)(-s);
+    } else {
+      const uint64_t i = (uint64_t)s >> 6;
+      const uint32_t sh = (uint32_t)(s & 63);
+      uint64_t x = i < nsw ? src[i] >> sh : 0ull;
+      if (sh && i + 1 < nsw) x |= src[i + 1] << (64 - sh);
+      v |= x;
+    }
+  }
+  const uint64_t lo = w << 6;
+  if (end < lo + 64) v &= (1ull << (end - lo)) - 1ull;  // end > lo here
+  dst[w] = v;
+}
+
 // ------------------------------------------------------------------------------------------------ stitch
 __global__ void k_stitch(uint64_t* __restrict__ dst, uint64_t off, const uint64_t* __restrict__ src, uint64_t bits)
 {
@@ -1288,6 +1324,15 @@ hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream)
 {
   k_set_u64<<<1, 1, 0, S(stream)>>>(p, v);
+  return hipGetLastError();
+}
+
+hipError_t launch_prepend_header(uint64_t* dst, uint32_t off, const uint64_t* src, const uint64_t* d_bits,
+                                 const uint64_t* header, uint64_t max_words, uint64_t* d_total, void* stream)
+{
+  const uint64_t grid = (max_words + 255) / 256;
+  k_prepend_header<<<(uint32_t)(grid ? grid : 1), 256, 0, S(stream)>>>(dst, off, src, d_bits, header[0], header[1],
+                                                                      header[2], d_total);
   return hipGetLastError();
 }
 

@@ -38,6 +38,8 @@ hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in
                          uint32_t chunk, uint64_t nchunks, bool fixed, uint64_t base_bits, uint64_t* end_out,
                          void* stream);
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
+hipError_t launch_prepend_header(uint64_t* dst, uint32_t off, const uint64_t* src, const uint64_t* d_bits,
+                                 const uint64_t* header, uint64_t max_words, uint64_t* d_total, void* stream);
 hipError_t launch_stitch(uint64_t* dst, uint64_t off, const uint64_t* src, uint64_t bits, void* stream);
 hipError_t launch_stage(int which, int dims, const void* a, const void* b, uint32_t n, void* out, uint32_t x0,
                         uint32_t x1, void* out2, uint32_t slot_words, void* stream);

@@ -13,8 +13,6 @@ PCIe copies per step. Two device-resident replacements:
 
 Both register with `ddp_model.register_comm_hook(GcowHookState(...), hook)`.
 """
-from __future__ import annotations
-
 from dataclasses import dataclass, field
 
 import torch
@@ -38,13 +36,13 @@ class GcowHookState:
         return self.encoders[key]
 
 
-def _done(t: torch.Tensor) -> torch.futures.Future:
+def _done(t: torch.Tensor) -> torch.futures.Future[torch.Tensor]:
     fut = torch.futures.Future()
     fut.set_result(t)
     return fut
 
 
-def roundtrip_hook(state: GcowHookState, bucket) -> torch.futures.Future:
+def roundtrip_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.Tensor]:
     """Mean all-reduce, then the lossy encode -> decode the reference applies (zfpy), device-resident."""
     group = state.process_group
     buf = bucket.buffer()
@@ -64,7 +62,7 @@ def roundtrip_hook(state: GcowHookState, bucket) -> torch.futures.Future:
     return fut.then(lossy)
 
 
-def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Future:
+def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.Tensor]:
     """Encode locally, all-gather compressed streams, decode every rank's stream and average."""
     group = state.process_group
     buf = bucket.buffer()

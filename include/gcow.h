@@ -237,6 +237,31 @@ gcow_status gcow_decode_device(const zfp_input* field, const gcow_params* p, con
 gcow_status gcow_stitch_device(uint64_t* d_dst, uint64_t dst_bit_offset, const uint64_t* d_src, uint64_t src_bits,
                                void* hip_stream);
 
+/*
+ * zfp 0.5.5 stream header: the byte format zfpy.compress_numpy writes (hw/models/train_imagenet.py:459-465 calls
+ * it), i.e. libzfp zfp_write_header(ZFP_HEADER_FULL): magic 'z','f','p' + codec version 5 (32 bits), field metadata
+ * (52 bits: sizes, dims - 1, type - 1) and the compression mode (12-bit short form for rate / precision /
+ * accuracy, else 64 bits). sw/ declares ZFP_HEADER_* (sw/include/common.h:16-21) but never writes a header.
+ * Header metadata records zfp_type_float for fp32 and bf16 inputs (bf16 is coded by exact widening).
+ */
+uint gcow_header_bits(const gcow_params* p); /* 96 or 148 */
+/* Host: write the header of (field shape, p) into words[0..3) (zeroed by the call); returns its bit count. */
+uint gcow_write_header(const zfp_input* field, const gcow_params* p, uint64_t* words);
+/* Host: parse a header (at least 3 words). Fills field->nx..nz and dtype (data/strides untouched) and p; returns
+ * the header bit count, 0 when the magic or version does not match or the type is not float. */
+uint gcow_read_header(const uint64_t* words, size_t nwords, zfp_input* field, gcow_params* p);
+/* Workspace for gcow_encode_device_zfp: the headerless stream plus gcow_encode_workspace_bytes(). */
+size_t gcow_encode_zfp_workspace_bytes(const zfp_input* field, const gcow_params* p);
+/* Device encode to a header-prefixed stream (byte-identical to zfpy.compress_numpy). Capacity:
+ * gcow_max_output_bytes() + 24. *d_total_bits (device, optional) = header bits + stream bits. */
+gcow_status gcow_encode_device_zfp(const zfp_input* field, const gcow_params* p, void* d_out, size_t out_capacity,
+                                   uint64_t* d_total_bits, void* d_workspace, size_t workspace_bytes,
+                                   void* hip_stream);
+/* Decode a stream whose first block starts at bit_offset (e.g. gcow_read_header()'s return value). */
+gcow_status gcow_decode_device_at(const zfp_input* field, const gcow_params* p, const void* d_in, size_t in_bytes,
+                                  uint64_t bit_offset, const uint64_t* d_index, uint32_t index_stride,
+                                  void* hip_stream);
+
 /* Per-stage batched device kernels (the hw/stages split, for parity bisection; sw/tests/test_stages.cpp). */
 gcow_status gcow_stage_emax_device(const float* d_blocks, uint32_t nblocks, uint32_t dims, int32_t* d_emax,
                                    void* hip_stream);

@@ -79,6 +79,15 @@ def lib():
         L.orc_set_precision.argtypes = [P(Params), C.c_uint]
         L.orc_gen_bump2d.argtypes = [P(C.c_float), C.c_size_t, C.c_int]
         L.orc_gen_normal.argtypes = [P(C.c_float), C.c_size_t, C.c_double, C.c_uint64, C.c_int]
+        L.orc_decompress_at.restype = C.c_uint64
+        L.orc_decompress_at.argtypes = L.orc_decompress.argtypes + [C.c_uint64]
+        L.orc_stitch.argtypes = [P(C.c_uint64), C.c_uint64, P(C.c_uint64), C.c_uint64]
+        L.orc_header_bits.restype = C.c_uint
+        L.orc_header_bits.argtypes = [P(Params)]
+        L.orc_write_header.restype = C.c_uint
+        L.orc_write_header.argtypes = [P(C.c_uint64), C.c_uint, P(C.c_size_t), C.c_uint, P(Params)]
+        L.orc_read_header.restype = C.c_uint
+        L.orc_read_header.argtypes = [P(C.c_uint64), P(C.c_uint), P(C.c_size_t), P(C.c_uint), P(Params)]
         _lib = L
     return _lib
 
@@ -270,3 +279,43 @@ def put_bits_header(words: np.ndarray, value: int, nbits: int, pos0: int = 0) ->
             p = pos0 + i
             words[p >> 6] |= np.uint64(1) << np.uint64(p & 63)
     return pos0 + nbits
+
+
+# ------------------------------------------------------------------ zfp 0.5.5 header (zfpy byte streams)
+def write_header(shape, p: Params, zfp_type: int = 3):
+    """Header words (3 x uint64) and bit count, as zfp_write_header(ZFP_HEADER_FULL)."""
+    dims, n = _shape(shape)
+    w = np.zeros(3, np.uint64)
+    bits = lib().orc_write_header(_p(w, C.c_uint64), dims, n, zfp_type, C.byref(p))
+    return w, int(bits)
+
+
+def read_header(words):
+    """-> (shape numpy-style, zfp_type, Params, header bits); header bits 0 when the magic does not match."""
+    w = np.zeros(3, np.uint64)
+    src = np.ascontiguousarray(words, dtype=np.uint64)[:3]
+    w[: len(src)] = src
+    dims, n, t, p = C.c_uint(), (C.c_size_t * 3)(), C.c_uint(), Params()
+    bits = lib().orc_read_header(_p(w, C.c_uint64), C.byref(dims), n, C.byref(t), C.byref(p))
+    shape = tuple(reversed([n[i] for i in range(dims.value)])) if bits else ()
+    return shape, t.value, p, int(bits)
+
+
+def compress_zfp(arr: np.ndarray, p: Params):
+    """zfpy.compress_numpy-style stream: header, then the blocks at the following bit, flushed to 64 bits."""
+    h, hb = write_header(arr.shape, p)
+    w, bits = compress(arr, p)
+    out = np.zeros((hb + bits + 63) // 64 + 1, np.uint64)
+    out[:3] |= h[:len(out[:3])]
+    lib().orc_stitch(_p(out, C.c_uint64), hb, _p(w, C.c_uint64), bits)
+    return out[: (hb + bits + 63) // 64].copy(), hb + bits
+
+
+def decompress_zfp(words: np.ndarray) -> np.ndarray:
+    shape, t, p, hb = read_header(words)
+    assert hb and t == 3, "not a float zfp stream"
+    dims, n = _shape(shape)
+    out = np.zeros(shape, dtype=np.float32)
+    w = np.concatenate([np.ascontiguousarray(words, dtype=np.uint64), np.zeros(2, np.uint64)])
+    lib().orc_decompress_at(_p(out, C.c_float), dims, n, None, C.byref(p), _p(w, C.c_uint64), len(w), hb)
+    return out

@@ -458,6 +458,8 @@ static void stitch(uint64_t* out, uint64_t off, const uint64_t* src, uint64_t bi
   }
 }
 
+void orc_stitch(uint64_t* out, uint64_t off, const uint64_t* src, uint64_t bits) { stitch(out, off, src, bits); }
+
 uint64_t orc_compress_mt(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
                          const orc_params* p, uint64_t* out, size_t out_words, int nthreads)
 {
@@ -581,6 +583,142 @@ uint64_t orc_decompress(float* data, unsigned dims, const size_t* n, const ptrdi
     scatter_block(f, data, dims, n, st, b);
   }
   return pos;
+}
+
+uint64_t orc_decompress_at(float* data, unsigned dims, const size_t* n, const ptrdiff_t* s, const orc_params* p,
+                           const uint64_t* in, size_t in_words, uint64_t start_bit)
+{
+  (void)in_words;
+  ptrdiff_t st[3];
+  default_strides(dims, n, s, st);
+  size_t nb = orc_num_blocks(dims, n);
+  uint64_t pos = start_bit;
+  float f[64];
+  size_t b[3];
+  for (size_t i = 0; i < nb; i++) {
+    block_coords(i, dims, n, b);
+    decode_fblock(in, &pos, p, f, dims);
+    scatter_block(f, data, dims, n, st, b);
+  }
+  return pos;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * zfp stream header (third-party format: LLNL zfp 0.5.5 src/zfp.c zfp_write_header / zfp_read_header,
+ * zfp_field_metadata, zfp_stream_mode, zfp_stream_set_mode; the format zfpy.compress_numpy writes, which the
+ * reference caller hw/models/train_imagenet.py:459-465 produces). Not implemented by sw/ (ZFP_HEADER_* in
+ * sw/include/common.h:16-21 are declared and unused). Pinned by libzfp-generated fixtures
+ * (tests/golden/libzfp_headers.json).
+ * ---------------------------------------------------------------------------------------------- */
+#define ORC_MIN_BITS 1u
+#define ORC_MAX_BITS 16657u
+#define ORC_MAX_PREC 64u
+#define ORC_MIN_EXP (-1074)
+
+static uint64_t field_meta(unsigned dims, const size_t* n, unsigned zfp_type)
+{
+  /* sizes (48 bits: 48 / 24 / 16 per axis by dims), then dims - 1 (2 bits), then type - 1 (2 bits) */
+  uint64_t meta = 0;
+  unsigned w = dims == 1 ? 48 : dims == 2 ? 24 : 16;
+  for (int a = (int)dims - 1; a >= 0; a--) meta = (meta << w) + (uint64_t)(n[a] - 1);
+  meta = (meta << 2) + (dims - 1);
+  meta = (meta << 2) + (zfp_type - 1);
+  return meta;
+}
+
+static uint64_t stream_mode(const orc_params* p)
+{
+  /* compression-mode classification (zfp_stream_compression_mode), then the short 12-bit forms for the three
+   * standard modes, else four packed fields + 0xfff */
+  const int valid = p->minbits <= p->maxbits && p->maxprec >= 1 && p->maxprec <= 64;
+  const int dflt = p->minbits == ORC_MIN_BITS && p->maxbits == ORC_MAX_BITS && p->maxprec == ORC_MAX_PREC &&
+                   p->minexp == ORC_MIN_EXP;
+  if (valid && !dflt) {
+    if (p->minbits == p->maxbits && p->maxbits >= 1 && p->maxbits <= ORC_MAX_BITS && p->maxprec >= ORC_MAX_PREC &&
+        p->minexp <= ORC_MIN_EXP) {
+      if (p->maxbits <= 2048) return (uint64_t)(p->maxbits - 1);
+    } else if (p->minbits <= ORC_MIN_BITS && p->maxbits >= ORC_MAX_BITS && p->maxprec >= 1 &&
+               p->minexp <= ORC_MIN_EXP) {
+      if (p->maxprec <= 128) return (uint64_t)(p->maxprec - 1) + 2048;
+    } else if (p->minbits <= ORC_MIN_BITS && p->maxbits >= ORC_MAX_BITS && p->maxprec >= ORC_MAX_PREC &&
+               p->minexp >= ORC_MIN_EXP) {
+      if (p->minexp <= 843) return (uint64_t)(p->minexp - ORC_MIN_EXP) + (2048 + 128 + 1);
+    }
+  }
+  uint64_t minbits = OMAX(1u, OMIN(p->minbits, 0x8000u)) - 1;
+  uint64_t maxbits = OMAX(1u, OMIN(p->maxbits, 0x8000u)) - 1;
+  uint64_t maxprec = OMAX(1u, OMIN(p->maxprec, 0x0080u)) - 1;
+  uint64_t minexp = (uint64_t)OMAX(0, OMIN(p->minexp + 16495, 0x7fff));
+  uint64_t mode = minexp;
+  mode = (mode << 7) + maxprec;
+  mode = (mode << 15) + maxbits;
+  mode = (mode << 15) + minbits;
+  mode = (mode << 12) + 0xfffu;
+  return mode;
+}
+
+unsigned orc_header_bits(const orc_params* p) { return stream_mode(p) < 0xfffu ? 96u : 148u; }
+
+unsigned orc_write_header(uint64_t* words, unsigned dims, const size_t* n, unsigned zfp_type, const orc_params* p)
+{
+  uint64_t pos = 0;
+  put_bits(words, &pos, 'z', 8);
+  put_bits(words, &pos, 'f', 8);
+  put_bits(words, &pos, 'p', 8);
+  put_bits(words, &pos, 5, 8); /* zfp_codec_version of zfp 0.5.5 */
+  put_bits(words, &pos, field_meta(dims, n, zfp_type), 52);
+  uint64_t mode = stream_mode(p);
+  put_bits(words, &pos, mode, mode < 0xfffu ? 12 : 64);
+  return (unsigned)pos;
+}
+
+unsigned orc_read_header(const uint64_t* words, unsigned* dims, size_t* n, unsigned* zfp_type, orc_params* p)
+{
+  uint64_t pos = 0;
+  if (get_bits(words, &pos, 8) != 'z' || get_bits(words, &pos, 8) != 'f' || get_bits(words, &pos, 8) != 'p' ||
+      get_bits(words, &pos, 8) != 5)
+    return 0;
+  uint64_t meta = get_bits(words, &pos, 52);
+  *zfp_type = (unsigned)(meta & 3u) + 1;
+  meta >>= 2;
+  *dims = (unsigned)(meta & 3u) + 1;
+  meta >>= 2;
+  unsigned w = *dims == 1 ? 48 : *dims == 2 ? 24 : 16;
+  for (unsigned a = 0; a < 3; a++) n[a] = 0;
+  if (*dims > 3) return 0;
+  for (unsigned a = 0; a < *dims; a++) {
+    n[a] = (size_t)(meta & ((1ull << w) - 1)) + 1;
+    meta >>= w;
+  }
+  uint64_t mode = get_bits(words, &pos, 12);
+  if (mode < 0xfffu) {
+    if (mode < 2048) {
+      p->minbits = p->maxbits = (unsigned)mode + 1;
+      p->maxprec = ORC_MAX_PREC;
+      p->minexp = ORC_MIN_EXP;
+    } else if (mode < 2048 + 128) {
+      p->minbits = ORC_MIN_BITS;
+      p->maxbits = ORC_MAX_BITS;
+      p->maxprec = (unsigned)mode + 1 - 2048;
+      p->minexp = ORC_MIN_EXP;
+    } else {
+      p->minbits = ORC_MIN_BITS;
+      p->maxbits = ORC_MAX_BITS;
+      p->maxprec = ORC_MAX_PREC;
+      p->minexp = (int)mode + ORC_MIN_EXP - (2048 + 128 + 1);
+    }
+  } else {
+    mode += get_bits(words, &pos, 52) << 12;
+    mode >>= 12;
+    p->minbits = (unsigned)(mode & 0x7fffu) + 1;
+    mode >>= 15;
+    p->maxbits = (unsigned)(mode & 0x7fffu) + 1;
+    mode >>= 15;
+    p->maxprec = (unsigned)(mode & 0x7fu) + 1;
+    mode >>= 7;
+    p->minexp = (int)(mode & 0x7fffu) - 16495;
+  }
+  return (unsigned)pos;
 }
 
 /* ------------------------------------------------------------------------------------------------

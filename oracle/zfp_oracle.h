@@ -64,6 +64,16 @@ void orc_block_bits(const void* data, int dtype, unsigned dims, const size_t* n,
 uint64_t orc_decompress(float* data, unsigned dims, const size_t* n, const ptrdiff_t* s, const orc_params* p,
                         const uint64_t* in, size_t in_words);
 
+uint64_t orc_decompress_at(float* data, unsigned dims, const size_t* n, const ptrdiff_t* s, const orc_params* p,
+                           const uint64_t* in, size_t in_words, uint64_t start_bit);
+/* OR `bits` bits of src into zeroed out[] at bit offset off (the multi-shard stream stitch). */
+void orc_stitch(uint64_t* out, uint64_t off, const uint64_t* src, uint64_t bits);
+
+/* ---- zfp 0.5.5 stream header (zfp_write_header / zfp_read_header, ZFP_HEADER_FULL) ---- */
+unsigned orc_header_bits(const orc_params* p);  /* 96 (short mode) or 148 */
+unsigned orc_write_header(uint64_t* words, unsigned dims, const size_t* n, unsigned zfp_type, const orc_params* p);
+unsigned orc_read_header(const uint64_t* words, unsigned* dims, size_t* n, unsigned* zfp_type, orc_params* p);
+
 /* ---- parameter helpers (common.c:6-21 accuracy; libzfp set_rate / set_precision) ---- */
 void orc_set_accuracy(orc_params* p, double tol);
 void orc_set_rate(orc_params* p, double rate, unsigned dims);

@@ -94,3 +94,35 @@ def test_shard_bounds_cover_and_align():
                 assert hi == lo2 and (lo % 4 == 0 or lo == hi == nvals)
             for lo, hi in b[:-1]:
                 assert (hi - lo) % 64 == 0 or hi == nvals  # 16 blocks: 64-bit aligned at rate >= 1/4
+
+
+
+def _ddp_register(rank, world, port, q):
+    import sys
+    import torch.nn as nn
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    try:
+        from gcow_amd import ddp
+        for h in (ddp.roundtrip_hook, ddp.compressed_allgather_hook):
+            m = nn.parallel.DistributedDataParallel(nn.Linear(4, 4))
+            m.register_comm_hook(ddp.GcowHookState(), h)  # DDP validates the hook signature here
+        q.put((rank, True))
+    except Exception as ex:
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_hooks_register():
+    """gcow_amd.ddp hooks pass DDP's comm-hook signature check (compute runs in the -m gpu DDP tests)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_register, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok is True for _, ok in res), res

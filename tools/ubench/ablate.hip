@@ -112,6 +112,334 @@ __global__ __launch_bounds__(256) void k_floor1(const float4* __restrict__ in, u
     else ((nu2*)out)[i] = w;
   }
 }
+// compute floor of the lean-3 coder: inputs re-read from a 1 MiB L2-resident window, results folded per lane
+template <int K>
+__global__ __launch_bounds__(256) void k_compute_floor(const float4* __restrict__ in, uint32_t nfull,
+                                                       uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  __syncthreads();
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  uint64_t accx = 0;
+  for (; b < nfull; b += stride) {
+    const float4 v = in[b & 0xffffu];
+    float f[4] = {v.x, v.y, v.z, v.w};
+    bool sp;
+    uint64_t w = encode_block1d_lean3<64>(f, tab2, sp);
+    if (K == 1 && sp) {
+      RegWriter64 rw{0ull, 0u};
+      Params p{64, 64, 64, -1074};
+      encode_block<1>(rw, f, p);
+      w = rw.acc;
+    }
+    accx ^= w + b;
+  }
+  out[blockIdx.x * 256u + threadIdx.x] = accx;
+}
+
+// timing-only variants of the lean-3 coder (outputs not exact unless noted):
+//   F & 1: group-phase LDS address independent of the previous lookup (latency chain removed)
+//   F & 2: no second plane window (Y2)
+//   F & 4: group phase skipped
+template <int F>
+__device__ __forceinline__ uint64_t lean3_var(const float* f, const uint32_t* tab2)
+{
+  const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
+  const uint32_t a2 = __float_as_uint(f[2]) & 0x7fffffffu, a3 = __float_as_uint(f[3]) & 0x7fffffffu;
+  const uint32_t m = max(max(a0, a1), max(a2, a3));
+  const bool special = m >= 0x7f800000u;
+  const bool zero = m == 0;
+  const uint32_t E = special ? 150u : (m >> 23);
+  const bool tiny = E < 29u;
+  const float s = __uint_as_float((283u - (tiny ? 150u : E)) << 23);
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = tiny ? (int32_t)0x80000000 : (int32_t)(f[i] * s);
+  fwd_lift(q[0], q[1], q[2], q[3]);
+  uint32_t u[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = ((uint32_t)q[i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+  uint64_t acc = 2ull * E + 3ull;
+  const int M0 = 31 - (int)__builtin_clz(u[0] | u[1] | u[2] | u[3] | 1u);
+  const int L3 = u[3] ? 31 - (int)__builtin_clz(u[3]) : -1;
+  uint32_t pos = 9 + (uint32_t)(31 - M0);
+  const uint64_t Y = plane_window(u, (uint32_t)(31 - M0));
+  const int jg = M0 - max(L3, 0);
+  uint32_t n = 0;
+  int jend = 0;
+  if constexpr (!(F & 4)) {
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      const bool act = (j <= jg) && (pos < 64);
+      if (!__any(act)) break;
+      const uint32_t b = (uint32_t)(Y >> (4 * j)) & 255u;
+      const uint32_t e = (F & 1) ? tab2[((j & 3) << 8) | b] : tab2[(n << 8) | b];
+      const uint32_t len = act ? ((e >> 14) & 15u) : 0u;
+      const uint64_t code = act ? (uint64_t)(e & 0x3fffu) : 0ull;
+      acc |= code << pos;
+      pos += len;
+      n = act ? (e >> 18) : n;
+      jend = act ? j + 2 : jend;
+    }
+  } else {
+    jend = (jg + 2) & ~1;
+    pos += 2 * jend;
+  }
+  if (pos < 64 && L3 >= 0 && jend < 16) {
+    uint64_t field = Y >> (4 * jend);
+    if (!(F & 2))
+      if (4u * (uint32_t)(16 - jend) < 64 - pos && M0 >= 16 && jend > 0)
+        field |= plane_window(u, (uint32_t)(31 - M0 + 16)) << (64 - 4 * jend);
+    acc |= field << pos;
+  }
+  acc = zero ? 0ull : acc;
+  return special ? 0ull : acc;
+}
+
+template <int F>
+__global__ __launch_bounds__(256) void k_var(const void* __restrict__ in, uint32_t nfull, uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  __syncthreads();
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  float cur[4], nxt[4];
+  if (b < nfull) load_row4_nt<DT_F32>(in, 4ll * b, cur);
+  for (; b < nfull; b += stride) {
+    const uint32_t bn = b + stride;
+    if (bn < nfull) load_row4_nt<DT_F32>(in, 4ll * bn, nxt);
+    const uint64_t w = lean3_var<F>(cur, tab2);
+    __builtin_nontemporal_store((unsigned long long)w, (unsigned long long*)out + b);
+#pragma unroll
+    for (int i = 0; i < 4; i++) cur[i] = nxt[i];
+  }
+}
+
+// exact: two blocks per lane per iteration (b and b + stride), lean-3 coder on each
+__global__ __launch_bounds__(256) void k_u2(const void* __restrict__ in, uint32_t nfull, Params p, uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  __syncthreads();
+  const uint32_t stride = gridDim.x * 512u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  float c0[4], c1[4], n0[4], n1[4];
+  if (b < nfull) load_row4_nt<DT_F32>(in, 4ll * b, c0);
+  if (b + stride / 2 < nfull) load_row4_nt<DT_F32>(in, 4ll * (b + stride / 2), c1);
+  for (; b < nfull; b += stride) {
+    const uint32_t bn = b + stride, b1 = b + stride / 2;
+    if (bn < nfull) load_row4_nt<DT_F32>(in, 4ll * bn, n0);
+    if (bn + stride / 2 < nfull) load_row4_nt<DT_F32>(in, 4ll * (bn + stride / 2), n1);
+    bool s0, s1;
+    uint64_t w0 = encode_block1d_lean3<64>(c0, tab2, s0);
+    uint64_t w1 = encode_block1d_lean3<64>(c1, tab2, s1);
+    if (s0) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, c0, p); w0 = rw.acc; }
+    if (s1) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, c1, p); w1 = rw.acc; }
+    __builtin_nontemporal_store((unsigned long long)w0, (unsigned long long*)out + b);
+    if (b1 < nfull) __builtin_nontemporal_store((unsigned long long)w1, (unsigned long long*)out + b1);
+#pragma unroll
+    for (int i = 0; i < 4; i++) { c0[i] = n0[i]; c1[i] = n1[i]; }
+  }
+}
+
+struct PlaneTab1 {
+  uint16_t v[80];
+};
+__host__ __device__ constexpr PlaneTab1 make_plane_tab1()
+{
+  PlaneTab1 T{};
+  for (uint32_t t = 0; t < 80; t++) T.v[t] = (uint16_t)plane_entry4_cx(t);
+  return T;
+}
+__device__ const PlaneTab1 g_plane_tab1 = make_plane_tab1();
+
+// exact lean coder with the one-plane table (80 x u16): code[0:7) | len[7:10) | n'[10:13)
+template <uint32_t WB>
+__device__ __forceinline__ uint64_t lean5(const float* f, const uint16_t* tab, bool& special)
+{
+  const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
+  const uint32_t a2 = __float_as_uint(f[2]) & 0x7fffffffu, a3 = __float_as_uint(f[3]) & 0x7fffffffu;
+  const uint32_t m = max(max(a0, a1), max(a2, a3));
+  special = m >= 0x7f800000u;
+  const bool zero = m == 0;
+  const uint32_t E = special ? 150u : (m >> 23);
+  const bool tiny = E < 29u;
+  const float s = __uint_as_float((283u - (tiny ? 150u : E)) << 23);
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = tiny ? (int32_t)0x80000000 : (int32_t)(f[i] * s);
+  fwd_lift(q[0], q[1], q[2], q[3]);
+  uint32_t u[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = ((uint32_t)q[i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+  uint64_t acc = 2ull * E + 3ull;
+  const int M0 = 31 - (int)__builtin_clz(u[0] | u[1] | u[2] | u[3] | 1u);
+  const int L3 = u[3] ? 31 - (int)__builtin_clz(u[3]) : -1;
+  uint32_t pos = 9 + (uint32_t)(31 - M0);
+  const uint64_t Y = plane_window(u, (uint32_t)(31 - M0));
+  const int jg = M0 - max(L3, 0);
+  uint32_t n = 0;
+  int jend = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const bool act = (j <= jg) && (pos < WB);
+    if (!__any(act)) break;
+    const uint32_t x = (uint32_t)(Y >> (4 * j)) & 15u;
+    const uint32_t e = tab[(n << 4) | x];
+    const uint32_t len = act ? ((e >> 7) & 7u) : 0u;
+    const uint64_t code = act ? (uint64_t)(e & 127u) : 0ull;
+    acc |= code << pos;
+    pos += len;
+    n = act ? (e >> 10) : n;
+    jend = act ? j + 1 : jend;
+  }
+  special = special || ((jend >= 16) && (jend <= jg) && (pos < WB));
+  if (pos < WB && L3 >= 0 && jend < 16) {
+    uint64_t field = Y >> (4 * jend);
+    if (4u * (uint32_t)(16 - jend) < WB - pos && M0 >= 16 && jend > 0)
+      field |= plane_window(u, (uint32_t)(31 - M0 + 16)) << (64 - 4 * jend);
+    acc |= field << pos;
+  } else if (pos < WB && L3 >= 0 && jend >= 16 && M0 >= 16) {
+    acc |= (plane_window(u, (uint32_t)(31 - M0 + 16)) >> (4 * (jend - 16))) << pos;
+  }
+  acc = zero ? 0ull : acc;
+  return WB == 64 ? acc : (acc & ((1ull << WB) - 1ull));
+}
+
+// non-persistent, K blocks per lane (lane t of WG g codes blocks g*256K + t + 256i), one-plane table
+template <int K>
+__global__ __launch_bounds__(256) void k_np1(const void* __restrict__ in, uint32_t nfull, Params p,
+                                              uint64_t* __restrict__ out)
+{
+  __shared__ uint16_t tab[80];
+  const uint32_t b0 = blockIdx.x * (256u * K) + threadIdx.x;
+  float f[K][4];
+#pragma unroll
+  for (int i = 0; i < K; i++)
+    if (b0 + 256u * i < nfull) load_row4_nt<DT_F32>(in, 4ll * (b0 + 256u * i), f[i]);
+  if (threadIdx.x < 80) tab[threadIdx.x] = g_plane_tab1.v[threadIdx.x];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < K; i++) {
+    const uint32_t b = b0 + 256u * i;
+    if (b >= nfull) break;
+    bool sp;
+    uint64_t w = lean5<64>(f[i], tab, sp);
+    if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, f[i], p); w = rw.acc; }
+    __builtin_nontemporal_store((unsigned long long)w, (unsigned long long*)out + b);
+  }
+}
+
+// persistent with the one-plane table (isolates the table size from the launch shape)
+__global__ __launch_bounds__(256) void k_p1(const void* __restrict__ in, uint32_t nfull, Params p,
+                                             uint64_t* __restrict__ out)
+{
+  __shared__ uint16_t tab[80];
+  if (threadIdx.x < 80) tab[threadIdx.x] = g_plane_tab1.v[threadIdx.x];
+  __syncthreads();
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  float cur[4], nxt[4];
+  if (b < nfull) load_row4_nt<DT_F32>(in, 4ll * b, cur);
+  for (; b < nfull; b += stride) {
+    const uint32_t bn = b + stride;
+    if (bn < nfull) load_row4_nt<DT_F32>(in, 4ll * bn, nxt);
+    bool sp;
+    uint64_t w = lean5<64>(cur, tab, sp);
+    if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, cur, p); w = rw.acc; }
+    __builtin_nontemporal_store((unsigned long long)w, (unsigned long long*)out + b);
+#pragma unroll
+    for (int i = 0; i < 4; i++) cur[i] = nxt[i];
+  }
+}
+
+// persistent, prefetch depth D (D iterations of loads in flight), lean-3 coder, exact
+template <int D>
+__global__ __launch_bounds__(256) void k_pd(const void* __restrict__ in, uint32_t nfull, Params p,
+                                             uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  float r[D + 1][4];
+#pragma unroll
+  for (int d = 0; d < D; d++)
+    if (b + d * stride < nfull) load_row4_nt<DT_F32>(in, 4ll * (b + d * stride), r[d]);
+  __syncthreads();
+  for (; b < nfull; b += stride) {
+    const uint32_t bn = b + D * stride;
+    if (bn < nfull) load_row4_nt<DT_F32>(in, 4ll * bn, r[D]);
+    bool sp;
+    uint64_t w = encode_block1d_lean3<64>(r[0], tab2, sp);
+    if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, r[0], p); w = rw.acc; }
+    __builtin_nontemporal_store((unsigned long long)w, (unsigned long long*)out + b);
+#pragma unroll
+    for (int d = 0; d < D; d++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) r[d][i] = r[d + 1][i];
+  }
+}
+
+// persistent, prefetch depth D with UNCONDITIONAL (index-clamped) prefetch loads, so the waitcnt pass can keep the
+// prefetches in flight (a conditional load forces s_waitcnt vmcnt(0) at the merge), lean-3 coder, exact
+template <int D>
+__global__ __launch_bounds__(256) void k_pdu(const void* __restrict__ in, uint32_t nfull, Params p,
+                                              uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t last = nfull - 1;
+  float r[D + 1][4];
+#pragma unroll
+  for (int d = 0; d < D; d++) load_row4_nt<DT_F32>(in, 4ll * min(b + d * stride, last), r[d]);
+  __syncthreads();
+  for (; b < nfull; b += stride) {
+    load_row4_nt<DT_F32>(in, 4ll * min(b + D * stride, last), r[D]);
+    bool sp;
+    uint64_t w = encode_block1d_lean3<64>(r[0], tab2, sp);
+    if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, r[0], p); w = rw.acc; }
+    __builtin_nontemporal_store((unsigned long long)w, (unsigned long long*)out + b);
+#pragma unroll
+    for (int d = 0; d < D; d++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) r[d][i] = r[d + 1][i];
+  }
+}
+
+// persistent, NB rotating register buffers without register moves (loop unrolled NB times), prefetch depth NB - 1
+template <int NB>
+__global__ __launch_bounds__(256) void k_rot(const void* __restrict__ in, uint32_t nfull, Params p,
+                                              uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t last = nfull - 1;
+  float r[NB][4];
+#pragma unroll
+  for (int d = 0; d < NB - 1; d++) load_row4_nt<DT_F32>(in, 4ll * min(b + d * stride, last), r[d]);
+  __syncthreads();
+  if (b >= nfull) return;
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      load_row4_nt<DT_F32>(in, 4ll * min(b + (NB - 1) * stride, last), r[(k + NB - 1) % NB]);
+      bool sp;
+      uint64_t w = encode_block1d_lean3<64>(r[k], tab2, sp);
+      if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, r[k], p); w = rw.acc; }
+      __builtin_nontemporal_store((unsigned long long)w, (unsigned long long*)out + b);
+      b += stride;
+      if (b >= nfull) return;
+    }
+  }
+}
 }  // namespace gcow
 
 extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, int wgs, void* stream)
@@ -128,6 +456,40 @@ extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, i
     case 6: gcow::k_floor2<true><<<min(grid, (nfull / 2 + 255) / 256), 256, 0, st>>>((const float4*)in, nfull / 2, (uint4*)out); break;
     case 7: gcow::k_floor1<false><<<grid, 256, 0, st>>>((const float4*)in, nfull, (uint2*)out); break;
     case 8: gcow::k_floor1<true><<<grid, 256, 0, st>>>((const float4*)in, nfull, (uint2*)out); break;
+    case 10: gcow::k_compute_floor<0><<<grid, 256, 0, st>>>((const float4*)in, nfull, (uint64_t*)out); break;
+    case 11: gcow::k_compute_floor<1><<<grid, 256, 0, st>>>((const float4*)in, nfull, (uint64_t*)out); break;
+    case 12: {
+      gcow::Params p{64, 64, 64, -1074};
+      gcow::k_encode_fixed1d_pnt<gcow::DT_F32, 64><<<grid, 256, 0, st>>>(in, nfull, p, out);
+      break;
+    }
+    case 13: gcow::k_var<1><<<grid, 256, 0, st>>>(in, nfull, (uint64_t*)out); break;
+    case 14: gcow::k_var<2><<<grid, 256, 0, st>>>(in, nfull, (uint64_t*)out); break;
+    case 15: gcow::k_var<4><<<grid, 256, 0, st>>>(in, nfull, (uint64_t*)out); break;
+    case 16: gcow::k_var<0><<<grid, 256, 0, st>>>(in, nfull, (uint64_t*)out); break;
+    case 17: gcow::k_var<7><<<grid, 256, 0, st>>>(in, nfull, (uint64_t*)out); break;
+    case 18: {
+      gcow::Params p{64, 64, 64, -1074};
+      gcow::k_u2<<<max(1u, grid / 2), 256, 0, st>>>(in, nfull, p, (uint64_t*)out);
+      break;
+    }
+    case 19: gcow::k_np1<1><<<(nfull + 255) / 256, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 20: gcow::k_np1<2><<<(nfull + 511) / 512, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 21: gcow::k_np1<4><<<(nfull + 1023) / 1024, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 22: gcow::k_p1<<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 23: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64><<<(nfull + 255) / 256, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 24: gcow::k_pd<2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 25: gcow::k_pd<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 26: gcow::k_pd<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 27: gcow::k_pd<6><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 28: gcow::k_pdu<1><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 29: gcow::k_pdu<2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 30: gcow::k_pdu<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 31: gcow::k_rot<2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 32: gcow::k_rot<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 33: gcow::k_rot<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 34: gcow::k_rot<6><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 35: gcow::k_rot<8><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
     case 9: gcow::k_floor1<false><<<(nfull + 255) / 256, 256, 0, st>>>((const float4*)in, nfull, (uint2*)out); break;
   }
   return (int)hipGetLastError();
