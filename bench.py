@@ -213,7 +213,7 @@ def main():
             cpu = {"error": repr(ex)}
 
     if rank == 0:
-        kname = "k_encode_fixed1d_pnt"
+        kname = "k_encode_fixed1d_pipe"
         traffic = load_pmc_traffic(kname, workload)
         line = {
             "metric": "GiB/s device-resident fp32->ZFP encode, 256Mi-float bucket, 1/2/4/8 GPU",

@@ -630,6 +630,60 @@ __device__ __forceinline__ uint64_t encode_block1d_lean3(const float* f, const u
   return WB == 64 ? acc : (acc & ((1ull << WB) - 1ull));
 }
 
+// Lean-4 block. Two facts shorten the wave-uniform group-test loop of lean-3:
+//  * with three coefficients significant (n = 3) a plane's code is its nibble verbatim: the three known bits, then
+//    the group test for coefficient 3 -- which is that coefficient's bit, its own 1 being implied (encode.c:318-333);
+//    so the group phase ends at plane T2 = max(L2, L3), not at L3;
+//  * lanes whose group phase is over keep looking up plane pairs: rows n >= 3 of the pair table are verbatim, so the
+//    extra iterations emit tail nibbles and the loop needs no per-lane activity masks; the tail then starts at the
+//    same (wave-uniform) window nibble for every lane.
+template <uint32_t WB>
+__device__ __forceinline__ uint64_t encode_block1d_lean4(const float* f, const uint32_t* tab2, bool& special)
+{
+  const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
+  const uint32_t a2 = __float_as_uint(f[2]) & 0x7fffffffu, a3 = __float_as_uint(f[3]) & 0x7fffffffu;
+  const uint32_t m = max(max(a0, a1), max(a2, a3));
+  special = m >= 0x7f800000u;  // Inf or NaN present
+  const bool zero = m == 0;
+  const uint32_t E = special ? 150u : (m >> 23);
+  const bool tiny = E < 29u;
+  const float s = __uint_as_float((283u - (tiny ? 150u : E)) << 23);
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = tiny ? (int32_t)0x80000000 : (int32_t)(f[i] * s);
+  fwd_lift(q[0], q[1], q[2], q[3]);
+  uint32_t u[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = ((uint32_t)q[i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+  uint64_t acc = 2ull * E + 3ull;
+  const uint32_t o23 = u[2] | u[3];
+  const int M0 = 31 - (int)__builtin_clz(u[0] | u[1] | o23 | 1u);
+  const int T2 = o23 ? 31 - (int)__builtin_clz(o23) : 0;  // group phase: planes M0 .. max(T2, 0)
+  uint32_t pos = 9 + (uint32_t)(31 - M0);
+  const uint64_t Y = plane_window(u, (uint32_t)(31 - M0));
+  const int jg = M0 - T2;
+  uint32_t n = 0;
+  int j = 0;
+#pragma unroll
+  for (; j < 16; j += 2) {
+    if (!__any(j <= jg)) break;
+    const uint32_t e = tab2[(n << 8) | ((uint32_t)(Y >> (4 * j)) & 255u)];
+    const uint32_t code = pos < WB ? (e & 0x3fffu) : 0u;  // 64-bit shifts wrap: nothing past the budget
+    acc |= (uint64_t)code << pos;
+    pos += (e >> 14) & 15u;
+    n = e >> 18;
+  }
+  special = special || (jg >= 16 && pos < WB);  // group phase runs past the 16-plane window (generic coder)
+  if (j < 16 && pos < WB) acc |= (Y >> (4 * j)) << pos;  // rest of the window, verbatim
+  const uint32_t p2 = pos + 4u * (uint32_t)(16 - j);        // where plane M0 - 16 lands
+  if (__any(p2 < WB && M0 >= 16)) {
+    const uint64_t Y2 = plane_window(u, (uint32_t)max(47 - M0, 0));  // planes M0 - 16 .. M0 - 31
+    if (p2 < WB && M0 >= 16) acc |= Y2 << p2;
+  }
+  acc = zero ? 0ull : acc;
+  return WB == 64 ? acc : (acc & ((1ull << WB) - 1ull));
+}
+
 template <uint32_t WB>
 __device__ __noinline__ uint64_t encode_block1d_slow(const float* f, const Params p)
 {
@@ -781,6 +835,118 @@ __global__ __launch_bounds__(256) void k_encode_fixed1d_pnt(const void* __restri
     else __builtin_nontemporal_store((uint32_t)w, (uint32_t*)out + b);
 #pragma unroll
     for (int i = 0; i < 4; i++) cur[i] = nxt[i];
+  }
+}
+
+// ---- hand-counted memory pipeline for the persistent fixed-rate 1-D encoder
+// Loads and stores are raw buffer instructions issued from inline asm, so the compiler's waitcnt pass does not see
+// them; the waits are counted here instead. (With compiler-tracked loads the conditional / loop-carried prefetch
+// collapsed to s_waitcnt vmcnt(0) at the loop head, i.e. every block waited for the previous block's store ack:
+// vmcnt counts stores and loads together, in issue order.) Out-of-range lanes read zeros and their stores are dropped
+// by the buffer range check (num_records), which keeps the loop exit wave-uniform and every step's op count fixed.
+typedef int pipe_v4i __attribute__((ext_vector_type(4)));
+typedef float pipe_v4f __attribute__((ext_vector_type(4)));
+typedef unsigned int pipe_v2u __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ pipe_v4i buf_rsrc(const void* p, uint32_t bytes)
+{
+  const uint64_t a = (uint64_t)p;
+  pipe_v4i r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)((uint32_t)(a >> 32) & 0xffffu);  // stride 0
+  r.z = (int)bytes;                             // num_records: range check in bytes
+  r.w = 0x00020000;                             // gfx9 dword-3 config (raw buffer, no swizzle)
+  return r;
+}
+
+template <int DT> struct PipeRow;
+template <> struct PipeRow<DT_F32> {
+  typedef pipe_v4f T;
+  static __device__ __forceinline__ T load(uint32_t off, pipe_v4i rs)
+  {
+    T v;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+    return v;
+  }
+  static __device__ __forceinline__ void unpack(const T& v, float* f) { f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w; }
+};
+template <> struct PipeRow<DT_BF16> {
+  typedef pipe_v2u T;
+  static __device__ __forceinline__ T load(uint32_t off, pipe_v4i rs)
+  {
+    T v;
+    asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+    return v;
+  }
+  static __device__ __forceinline__ void unpack(const T& v, float* f)
+  {
+    f[0] = __uint_as_float(v.x << 16);
+    f[1] = __uint_as_float(v.x & 0xffff0000u);
+    f[2] = __uint_as_float(v.y << 16);
+    f[3] = __uint_as_float(v.y & 0xffff0000u);
+  }
+};
+
+template <int N, typename T>
+__device__ __forceinline__ void pipe_wait(T& v)
+{
+  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "n"(N) : "memory");  // ties v's uses to after the wait
+}
+
+template <uint32_t WB>
+__device__ __forceinline__ void pipe_store(uint32_t off, pipe_v4i rs, uint64_t w)
+{
+  if constexpr (WB == 64)
+    asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen nt" : : "v"(w), "v"(off), "s"(rs) : "memory");
+  else
+    asm volatile("buffer_store_dword %0, %1, %2, 0 offen nt" : : "v"((uint32_t)w), "v"(off), "s"(rs) : "memory");
+}
+
+// Persistent grid-stride encoder with NB rotating register buffers (prefetch depth NB): each step codes buffer k,
+// stores the block, then refills buffer k with the block NB strides ahead. In steady state the block coded next was
+// loaded NB steps ago and 2 (NB - 1) memory ops were issued after it, hence vmcnt(2 (NB - 1)). The caller keeps
+// (nfull + NB * stride) * bytes-per-block below 2^32 (chunked launches).
+template <int DT, uint32_t WB, int NB>
+__global__ __launch_bounds__(256) void k_encode_fixed1d_pipe(const void* __restrict__ in, uint32_t nfull, Params p,
+                                                             void* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+#pragma unroll
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  __syncthreads();
+  constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;  // input bytes per block
+  const pipe_v4i rin = buf_rsrc(in, nfull * IB), rout = buf_rsrc(out, nfull * (WB / 8));
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  uint32_t bw = __builtin_amdgcn_readfirstlane(blockIdx.x * 256u + (threadIdx.x & ~63u));  // wave's first block
+  if (bw >= nfull) return;
+  typename PipeRow<DT>::T r[NB];
+#pragma unroll
+  for (int d = 0; d < NB; d++) r[d] = PipeRow<DT>::load((b + d * stride) * IB, rin);
+#pragma unroll
+  for (int d = 0; d < NB; d++) pipe_wait<0>(r[d]);
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      pipe_wait<2 * (NB - 1)>(r[k]);
+      float f[4];
+      PipeRow<DT>::unpack(r[k], f);
+      bool special;
+      uint64_t w = encode_block1d_lean4<WB>(f, tab2, special);
+      if (special) {
+        RegWriter64 rw{0ull, 0u};
+        encode_block<1>(rw, f, p);
+        w = WB == 64 ? rw.acc : (rw.acc & ((1ull << WB) - 1ull));
+      }
+      pipe_store<WB>(b * (WB / 8), rout, w);
+      r[k] = PipeRow<DT>::load((b + NB * stride) * IB, rin);
+      b += stride;
+      bw += stride;
+      if (bw >= nfull) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+      }
+    }
   }
 }
 
@@ -1209,15 +1375,15 @@ static int fixed1d_variant()
 {
   if (g_fixed1d_variant < 0) {
     const char* e = getenv("GCOW_FIXED1D_VARIANT");
-    g_fixed1d_variant = e ? atoi(e) : 8;
+    g_fixed1d_variant = e ? atoi(e) : 9;
   }
   return g_fixed1d_variant;
 }
 
-static int fixed1d_wgs_per_cu()
+static int fixed1d_wgs_per_cu(int dflt = 32)
 {
   const char* e = getenv("GCOW_FIXED1D_WGS");
-  return e ? atoi(e) : 32;
+  return e ? atoi(e) : dflt;
 }
 
 template <int DT, uint32_t WB>
@@ -1246,9 +1412,20 @@ static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, vo
       k_encode_fixed1d_l3<DT, WB><<<g6, 256, 0, st>>>(in, nfull, p, out);
     } else if (v == 7) {
       k_encode_fixed1d_np<DT, WB><<<(nfull + 255) / 256, 256, 0, st>>>(in, nfull, p, out);
-    } else {
+    } else if (v == 8) {
       const uint32_t g8 = min((nfull + 255) / 256, (uint32_t)(256 * fixed1d_wgs_per_cu()));
       k_encode_fixed1d_pnt<DT, WB><<<g8, 256, 0, st>>>(in, nfull, p, out);
+    } else {
+      // chunks keep every buffer offset (block + NB * stride) * 16 below 2^32
+      constexpr uint32_t CH = 1u << 27;
+      constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;
+      const uint32_t wgs = (uint32_t)fixed1d_wgs_per_cu(12);
+      for (uint32_t c0 = 0; c0 < nfull; c0 += CH) {
+        const uint32_t nc = min(CH, nfull - c0);
+        const uint32_t g9 = min((nc + 255) / 256, (uint32_t)(256 * wgs));
+        k_encode_fixed1d_pipe<DT, WB, 3><<<g9, 256, 0, st>>>((const char*)in + (size_t)c0 * IB, nc, p,
+                                                             (char*)out + (size_t)c0 * (WB / 8));
+      }
     }
   }
   if (nvals % 4) k_encode_fixed1d_tail<DT, WB><<<1, 128, 0, st>>>(in, nvals, nfull, p, out);

@@ -440,6 +440,207 @@ __global__ __launch_bounds__(256) void k_rot(const void* __restrict__ in, uint32
     }
   }
 }
+
+// as k_rot, but each step refills the buffer it just coded (after its store): no load at the loop head
+template <int NB>
+__global__ __launch_bounds__(256) void k_rot2(const void* __restrict__ in, uint32_t nfull, Params p,
+                                               uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t last = nfull - 1;
+  float r[NB][4];
+#pragma unroll
+  for (int d = 0; d < NB; d++) load_row4_nt<DT_F32>(in, 4ll * min(b + d * stride, last), r[d]);
+  __syncthreads();
+  if (b >= nfull) return;
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      bool sp;
+      uint64_t w = encode_block1d_lean3<64>(r[k], tab2, sp);
+      if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, r[k], p); w = rw.acc; }
+      __builtin_nontemporal_store((unsigned long long)w, (unsigned long long*)out + b);
+      load_row4_nt<DT_F32>(in, 4ll * min(b + NB * stride, last), r[k]);
+      b += stride;
+      if (b >= nfull) return;
+    }
+  }
+}
+
+// k_rot2 + explicit counted waits at the loop edges so that the loop header needs no wait of its own
+template <int NB>
+__global__ __launch_bounds__(256) void k_rot3(const void* __restrict__ in, uint32_t nfull, Params p,
+                                               uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t last = nfull - 1;
+  float r[NB][4];
+#pragma unroll
+  for (int d = 0; d < NB; d++) load_row4_nt<DT_F32>(in, 4ll * min(b + d * stride, last), r[d]);
+  __syncthreads();
+  if (b >= nfull) return;
+  __builtin_amdgcn_s_waitcnt(0xF70 | (NB - 1));  // r[0] landed
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      bool sp;
+      uint64_t w = encode_block1d_lean3<64>(r[k], tab2, sp);
+      if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, r[k], p); w = rw.acc; }
+      __builtin_nontemporal_store((unsigned long long)w, (unsigned long long*)out + b);
+      load_row4_nt<DT_F32>(in, 4ll * min(b + NB * stride, last), r[k]);
+      b += stride;
+      if (b >= nfull) return;
+    }
+    __builtin_amdgcn_s_waitcnt(0xF70 | (2 * (NB - 1)));  // r[0] (refilled in step 0) landed
+  }
+}
+
+// k_rot2 with a wave-uniform loop exit (scalar trip test on the wave's first block), predicated store
+template <int NB>
+__global__ __launch_bounds__(256) void k_rot4(const void* __restrict__ in, uint32_t nfull, Params p,
+                                               uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  uint32_t bw = __builtin_amdgcn_readfirstlane(blockIdx.x * 256u + (threadIdx.x & ~63u));
+  const uint32_t last = nfull - 1;
+  float r[NB][4];
+#pragma unroll
+  for (int d = 0; d < NB; d++) load_row4_nt<DT_F32>(in, 4ll * min(b + d * stride, last), r[d]);
+  __syncthreads();
+  if (bw >= nfull) return;
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      bool sp;
+      uint64_t w = encode_block1d_lean3<64>(r[k], tab2, sp);
+      if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, r[k], p); w = rw.acc; }
+      if (b < nfull) __builtin_nontemporal_store((unsigned long long)w, (unsigned long long*)out + b);
+      load_row4_nt<DT_F32>(in, 4ll * min(b + NB * stride, last), r[k]);
+      b += stride;
+      bw += stride;
+      if (bw >= nfull) return;
+    }
+  }
+}
+
+// Hand-counted memory pipeline: buffer loads/stores issued by inline asm (invisible to the compiler's waitcnt pass)
+// with explicit s_waitcnt vmcnt(2 (NB - 1)) per step; out-of-range lanes load zeros / their stores are dropped by the
+// buffer range check, so the loop exit is wave-uniform and every step issues exactly one load and one store.
+typedef int abl_v4i __attribute__((ext_vector_type(4)));
+typedef float abl_v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ abl_v4i abl_rsrc(const void* p, uint32_t bytes)
+{
+  const uint64_t a = (uint64_t)p;
+  abl_v4i r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)((uint32_t)(a >> 32) & 0xffffu);
+  r.z = (int)bytes;
+  r.w = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ abl_v4f abl_load(uint32_t off, abl_v4i rs)
+{
+  abl_v4f v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+  return v;
+}
+__device__ __forceinline__ void abl_store(uint32_t off, abl_v4i rs, uint64_t w)
+{
+  asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen nt" : : "v"(w), "v"(off), "s"(rs) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void abl_wait(abl_v4f& v)
+{
+  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "n"(N) : "memory");
+}
+
+template <int NB, int MODE = 0>
+__global__ __launch_bounds__(256) void k_asm(const void* __restrict__ in, uint32_t nfull, Params p,
+                                              uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  __syncthreads();
+  const abl_v4i rin = abl_rsrc(in, nfull * 16u), rout = abl_rsrc(out, nfull * 8u);
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  uint32_t bw = __builtin_amdgcn_readfirstlane(blockIdx.x * 256u + (threadIdx.x & ~63u));
+  if (bw >= nfull) return;
+  abl_v4f r[NB];
+#pragma unroll
+  for (int d = 0; d < NB; d++) r[d] = abl_load((b + d * stride) * 16u, rin);
+#pragma unroll
+  for (int d = 0; d < NB; d++) abl_wait<0>(r[d]);
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      abl_wait<2 * (NB - 1)>(r[k]);
+      float f[4] = {r[k].x, r[k].y, r[k].z, r[k].w};
+      bool sp;
+      uint64_t w;
+      if constexpr (MODE == 2) {
+        w = (uint64_t)(__float_as_uint(f[0]) ^ __float_as_uint(f[1])) |
+            ((uint64_t)(__float_as_uint(f[2]) ^ __float_as_uint(f[3])) << 32);
+      } else {
+        w = encode_block1d_lean3<64>(f, tab2, sp);
+        if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, f, p); w = rw.acc; }
+      }
+      const uint32_t sb = MODE == 1 ? (b & 0xffffu) : b;  // MODE 1: L2-resident working set (compute floor)
+      const uint32_t lb = MODE == 1 ? ((b + NB * stride) & 0xffffu) : (b + NB * stride);
+      abl_store(sb * 8u, rout, w);
+      r[k] = abl_load(lb * 16u, rin);
+      b += stride;
+      bw += stride;
+      if (bw >= nfull) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+      }
+    }
+  }
+}
+
+// pure compute floor: each lane loads NB blocks once and re-encodes them for the wave's whole trip count
+// (same number of encodes as the real kernel, no per-iteration memory traffic), one store per lane at the end
+template <int NB>
+__global__ __launch_bounds__(256) void k_cfloor(const void* __restrict__ in, uint32_t nfull, Params p,
+                                                 uint64_t* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  __syncthreads();
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  uint32_t bw = __builtin_amdgcn_readfirstlane(blockIdx.x * 256u + (threadIdx.x & ~63u));
+  if (bw >= nfull) return;
+  float r[NB][4];
+#pragma unroll
+  for (int d = 0; d < NB; d++) load_row4_nt<DT_F32>(in, 4ll * min(b + d * stride, nfull - 1), r[d]);
+  uint64_t accx = 0;
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      bool sp;
+      uint64_t w = encode_block1d_lean3<64>(r[k], tab2, sp);
+      if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, r[k], p); w = rw.acc; }
+      accx ^= w;
+      r[k][0] = __uint_as_float(__float_as_uint(r[k][0]) ^ (uint32_t)(w & 1));  // keep the loop honest
+      bw += stride;
+      if (bw >= nfull) {
+        out[blockIdx.x * 256u + threadIdx.x] = accx;
+        return;
+      }
+    }
+  }
+}
 }  // namespace gcow
 
 extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, int wgs, void* stream)
@@ -490,6 +691,24 @@ extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, i
     case 33: gcow::k_rot<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
     case 34: gcow::k_rot<6><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
     case 35: gcow::k_rot<8><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 36: gcow::k_rot2<2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 37: gcow::k_rot2<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 38: gcow::k_rot2<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 39: gcow::k_rot3<2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 40: gcow::k_rot3<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 41: gcow::k_rot3<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 42: gcow::k_rot4<2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 43: gcow::k_rot4<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 44: gcow::k_rot4<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 45: gcow::k_asm<2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 46: gcow::k_asm<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 47: gcow::k_asm<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 48: gcow::k_asm<3, 1><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 49: gcow::k_asm<3, 2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 50: gcow::k_cfloor<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 51: gcow::k_encode_fixed1d_pipe<gcow::DT_F32, 64, 3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 52: gcow::k_encode_fixed1d_pipe<gcow::DT_F32, 64, 2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 53: gcow::k_encode_fixed1d_pipe<gcow::DT_F32, 64, 4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 9: gcow::k_floor1<false><<<(nfull + 255) / 256, 256, 0, st>>>((const float4*)in, nfull, (uint2*)out); break;
   }
   return (int)hipGetLastError();
