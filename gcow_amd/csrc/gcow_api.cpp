@@ -190,6 +190,11 @@ gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void
   if (!d_in) return fail(GCOW_ERR_INVALID, "null input stream");
   if (F.nblocks == 0) return GCOW_OK;
   const bool fixed = p->minbits == p->maxbits;
+  if (fixed && F.dims == 1 && F.vec && (p->maxbits == 64 || p->maxbits == 32) && p->maxprec >= 32 &&
+      p->minexp <= -154 && base_bits % 32 == 0 && !d_end && !getenv("GCOW_GENERIC_DECODE")) {
+    GCOW_HIP(gcow::launch_decode_fixed1d(F, P(*p), (const uint64_t*)d_in, base_bits, stream));
+    return GCOW_OK;
+  }
   uint32_t chunk;
   uint64_t nchunks;
   if (fixed) {

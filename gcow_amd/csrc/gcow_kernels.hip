@@ -847,6 +847,7 @@ __global__ __launch_bounds__(256) void k_encode_fixed1d_pnt(const void* __restri
 typedef int pipe_v4i __attribute__((ext_vector_type(4)));
 typedef float pipe_v4f __attribute__((ext_vector_type(4)));
 typedef unsigned int pipe_v2u __attribute__((ext_vector_type(2)));
+typedef unsigned int pipe_v4u __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ pipe_v4i buf_rsrc(const void* p, uint32_t bytes)
 {
@@ -1176,6 +1177,201 @@ __global__ __launch_bounds__(64) void k_decode(FieldDesc F, Params p, const uint
   if (end_out && c == nchunks - 1) *end_out = r.pos;
 }
 
+// ------------------------------------------------------------------------------------------------ fast 1-D decode
+// Fixed-rate 1-D decoder for whole-word blocks (maxbits 64 / 32, kmin = 0), the inverse of the lean-4 encoder:
+//  * header: bit 0 = 0 -> zero block; else biased emax in bits 1..8;
+//  * the empty planes above M0 are single '0' bits, so M0 = 31 - ctz(word >> 9);
+//  * group phase: one stream-window lookup per plane in a (n, next 7 bits) -> (nibble, length, n') table that
+//    restates libzfp decode_ints' unary run-length decode (decode.c:156-189 with the block-size fix); rows n >= 3
+//    are verbatim nibbles, so a wave-uniform loop runs until every lane has n >= 3 and the rest is a contiguous
+//    nibble run taken straight from the word;
+//  * the nibble window is turned back into four coefficients by the inverse 4 x 16 bit transpose.
+// A lane whose group phase runs past the 16-plane window falls back to the generic decoder.
+// Entry (n, r, b): decode one plane from state n with the next 7 stream bits b of which only r + 1 are inside the
+// block's bit budget (r = 7: at least 8). The budget matters exactly like libzfp's: when it runs out inside the
+// unary scan, decode_ints still deposits the coefficient at the current n (x += 1 << n++ after the inner loop).
+struct DecTab1 {
+  uint16_t v[5 * 8 * 128];
+};
+
+__host__ __device__ constexpr uint32_t dec_plane_cx(uint32_t t)
+{
+  const uint32_t n0 = t >> 10, r = (t >> 7) & 7u, b = t & 127u;
+  uint32_t n = n0, bits = r + 1, pos = 0, x = 0;
+  if (n >= 4) {  // verbatim nibble (zero past the budget)
+    const uint32_t m = bits < 4 ? bits : 4;
+    return (b & ((1u << m) - 1u)) | (m << 4) | (4u << 8);
+  }
+  const uint32_t m = n < bits ? n : bits;  // first n bits verbatim
+  x = b & ((1u << m) - 1u);
+  pos = m;
+  bits -= m;
+  while (n < 4 && bits) {
+    bits--;
+    if (!((b >> pos++) & 1u)) break;  // group test
+    while (n < 3 && bits) {
+      bits--;
+      if ((b >> pos++) & 1u) break;
+      n++;
+    }
+    x += 1u << n;
+    n++;
+  }
+  return x | (pos << 4) | (n << 8);
+}
+
+__host__ __device__ constexpr DecTab1 make_dec_tab1()
+{
+  DecTab1 T{};
+  for (uint32_t t = 0; t < 5 * 8 * 128; t++) T.v[t] = (uint16_t)dec_plane_cx(t);
+  return T;
+}
+
+__device__ const DecTab1 g_dec_tab1 = make_dec_tab1();
+
+__device__ __forceinline__ uint64_t inv_transpose4x16(uint64_t x)
+{
+  x = dswap64(x, 0x00000000FF00FF00ull, 24);
+  x = dswap64(x, 0x0000F0F00000F0F0ull, 12);
+  x = dswap64(x, 0x00000000CCCCCCCCull, 30);
+  x = dswap64(x, 0x0000AAAA0000AAAAull, 15);
+  return x;
+}
+
+// coefficient i's bits for 16 planes starting at plane `top` going down, from a nibble window
+__device__ __forceinline__ void window_to_coeffs(uint64_t Y, int top, uint32_t* u)
+{
+  const uint64_t x = inv_transpose4x16(Y);
+  const uint32_t sh = (uint32_t)(31 - top);
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] |= __builtin_bitreverse32((uint32_t)(x >> (16 * i)) & 0xffffu) >> sh;
+}
+
+template <uint32_t WB>
+__device__ __forceinline__ void decode_block1d_fast(uint64_t w, const uint16_t* dtab, float* f, bool& special)
+{
+  const bool nonzero = w & 1u;
+  const int emax = (int)((w >> 1) & 255u) - 127;
+  const uint64_t r = w >> 9;
+  const int z = r ? (int)__builtin_ctzll(r) : 64;
+  const int M0 = 31 - z;  // < 0: every coded plane empty
+  uint32_t pos = 9u + (uint32_t)z;
+  uint64_t Y = 0;
+  uint32_t n = 0;
+  int j = 0;
+#pragma unroll
+  for (; j < 16; j++) {
+    if (!__any(n < 3 && pos < WB && j <= M0)) break;
+    const uint32_t b7 = pos < WB ? (uint32_t)(w >> pos) & 127u : 0u;
+    const uint32_t rb = min(WB - pos, 8u) - 1u;  // budget bits left in this plane (pos >= WB: b7 = 0, any row)
+    const uint32_t e = dtab[(((n << 3) | rb) << 7) | b7];
+    Y |= (uint64_t)(e & 15u) << (4 * j);
+    pos += (e >> 4) & 15u;
+    n = e >> 8;
+  }
+  special = n < 3 && pos < WB && j <= M0;  // still in the group phase after 16 planes
+  if (j < 16 && pos < WB) Y |= (w >> pos) << (4 * j);  // verbatim nibbles (bits past the word are zero)
+  uint32_t u[4] = {0, 0, 0, 0};
+  if (M0 >= 0) {
+    window_to_coeffs(Y, M0, u);
+    const uint32_t p2 = pos + 4u * (uint32_t)(16 - j);  // stream position of plane M0 - 16
+    if (__any(p2 < WB && M0 >= 16)) {
+      const uint64_t Y2 = p2 < WB && M0 >= 16 ? w >> p2 : 0ull;
+      if (M0 >= 16) window_to_coeffs(Y2, M0 - 16, u);
+    }
+  }
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = (int32_t)((u[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+  inv_lift(q[0], q[1], q[2], q[3]);
+  const float sc = dequant_scale(emax);
+#pragma unroll
+  for (int i = 0; i < 4; i++) f[i] = nonzero ? sc * (float)q[i] : 0.0f;  // header bit 0: +0 whatever follows
+}
+
+template <uint32_t WB> struct PipeWord;
+template <> struct PipeWord<64> {
+  typedef pipe_v2u T;
+  static __device__ __forceinline__ T load(uint32_t off, pipe_v4i rs)
+  {
+    T v;
+    asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+    return v;
+  }
+  static __device__ __forceinline__ uint64_t get(const T& v) { return (uint64_t)v.x | ((uint64_t)v.y << 32); }
+};
+template <> struct PipeWord<32> {
+  typedef uint32_t T;
+  static __device__ __forceinline__ T load(uint32_t off, pipe_v4i rs)
+  {
+    T v;
+    asm volatile("buffer_load_dword %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+    return v;
+  }
+  static __device__ __forceinline__ uint64_t get(const T& v) { return (uint64_t)v; }
+};
+
+// Persistent fixed-rate 1-D decoder over full blocks [0, nfull) of a contiguous fp32 output, same hand-counted
+// pipeline as k_encode_fixed1d_pipe (one word load and one 16-B store per step).
+template <uint32_t WB, int NB>
+__global__ __launch_bounds__(256) void k_decode_fixed1d_pipe(const void* __restrict__ in, uint32_t nfull, Params p,
+                                                             float* __restrict__ out, uint64_t base_bits)
+{
+  __shared__ uint16_t dtab[5 * 8 * 128];
+  for (uint32_t t = threadIdx.x; t < 5 * 8 * 128 / 2; t += 256)  // 10 KiB, copied as dwords
+    ((uint32_t*)dtab)[t] = ((const uint32_t*)g_dec_tab1.v)[t];
+  __syncthreads();
+  constexpr uint32_t WBYTES = WB / 8;
+  // the caller guarantees base_bits % 32 == 0 (whole dwords: headerless streams and the 96-bit zfp header)
+  const pipe_v4i rin = buf_rsrc((const char*)in + base_bits / 8, nfull * WBYTES);
+  const __amdgpu_buffer_rsrc_t rout_b = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(nfull * 16u), 0x00020000);
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  uint32_t bw = __builtin_amdgcn_readfirstlane(blockIdx.x * 256u + (threadIdx.x & ~63u));
+  if (bw >= nfull) return;
+  typename PipeWord<WB>::T r[NB];
+#pragma unroll
+  for (int d = 0; d < NB; d++) r[d] = PipeWord<WB>::load((b + d * stride) * WBYTES, rin);
+#pragma unroll
+  for (int d = 0; d < NB; d++) pipe_wait<0>(r[d]);
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      pipe_wait<2 * (NB - 1)>(r[k]);
+      float f[4];
+      bool special;
+      decode_block1d_fast<WB>(PipeWord<WB>::get(r[k]), dtab, f, special);
+      if (special && b < nfull) {
+        BitReader rd{(const uint64_t*)in, base_bits + (uint64_t)b * WB};
+        decode_block<1>(rd, p, f);
+      }
+      pipe_v4u v;
+      v.x = __float_as_uint(f[0]); v.y = __float_as_uint(f[1]); v.z = __float_as_uint(f[2]); v.w = __float_as_uint(f[3]);
+      // 16-B store through the compiler (it inserts the VALU-write -> wide-store wait states that an inline-asm
+      // store would need by hand; with an asm store lanes 12-15 of each row stored stale data). It still counts in
+      // vmcnt exactly once per step, as the hand-counted waits assume; aux 2 = non-temporal.
+      __builtin_amdgcn_raw_buffer_store_b128(v, rout_b, (int)(b * 16u), 0, 2);
+      r[k] = PipeWord<WB>::load((b + NB * stride) * WBYTES, rin);
+      b += stride;
+      bw += stride;
+      if (bw >= nfull) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+      }
+    }
+  }
+}
+
+// the partial last block of a 1-D field (generic decoder, one lane)
+__global__ void k_decode_tail1d(FieldDesc F, Params p, const uint64_t* __restrict__ in, uint64_t base_bits,
+                                uint32_t b)
+{
+  BitReader r{in, base_bits + (uint64_t)b * p.maxbits};
+  float f[4];
+  decode_block<1>(r, p, f);
+  scatter_block<1>(F, b, f);
+}
+
 __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 
 // ------------------------------------------------------------------------------------------------ header stream
@@ -1495,6 +1691,24 @@ hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in
   if (F.dims == 1) k_decode<1><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
   else if (F.dims == 2) k_decode<2><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
   else k_decode<3><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t base_bits,
+                                 void* stream)
+{
+  const uint32_t nfull = (uint32_t)(F.n[0] / 4);
+  constexpr uint32_t CH = 1u << 27;
+  const uint32_t wgs = (uint32_t)fixed1d_wgs_per_cu(12);
+  for (uint32_t c0 = 0; c0 < nfull; c0 += CH) {
+    const uint32_t nc = min(CH, nfull - c0);
+    const uint32_t g = min((nc + 255) / 256, 256u * wgs);
+    float* out = (float*)F.data + (size_t)c0 * 4;
+    const uint64_t bb = base_bits + (uint64_t)c0 * p.maxbits;
+    if (p.maxbits == 64) k_decode_fixed1d_pipe<64, 3><<<g, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+    else k_decode_fixed1d_pipe<32, 3><<<g, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+  }
+  if (F.n[0] % 4) k_decode_tail1d<<<1, 1, 0, S(stream)>>>(F, p, in, base_bits, nfull);
   return hipGetLastError();
 }
 

@@ -37,6 +37,10 @@ hipError_t launch_encode_tiles(const FieldDesc& F, const Params& p, const TilePl
 hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
                          uint32_t chunk, uint64_t nchunks, bool fixed, uint64_t base_bits, uint64_t* end_out,
                          void* stream);
+// fixed-rate 1-D whole-word blocks (maxbits 64 / 32, maxprec >= 32, minexp <= -154), contiguous fp32 output,
+// base_bits % 32 == 0
+hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t base_bits,
+                                 void* stream);
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
 hipError_t launch_prepend_header(uint64_t* dst, uint32_t off, const uint64_t* src, const uint64_t* d_bits,
                                  const uint64_t* header, uint64_t max_words, uint64_t* d_total, void* stream);

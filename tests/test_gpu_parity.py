@@ -470,3 +470,22 @@ def test_ddp_hooks_single_rank(gc, orc, hook, mode):
             assert err <= 1e-6
         else:
             assert err <= 2.0 ** -10 * max(scale, 1e-30)  # 16 bits/value on smooth-ish gradients
+
+
+@pytest.mark.parametrize("r", [16, 8])
+def test_fast1d_decode_arbitrary_streams(gc, orc, r):
+    """The 1-D fixed-rate decoder on arbitrary bit patterns (not only encoder output): every header exponent, long
+    runs of empty planes, group phases that never reach n = 3, all-verbatim words; bit-exact vs libzfp semantics."""
+    rng = np.random.default_rng(5 + r)
+    nw = (1 << 16) * r // 64
+    w = rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64) * np.uint64(2) + rng.integers(0, 2, nw).astype(np.uint64)
+    # sparse words: long zero runs after the header
+    sparse = w & (rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64) & rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64))
+    words = np.concatenate([w, sparse | np.uint64(0x0101010101010101)])
+    n = words.size * 64 // r
+    op = orc.rate(r, 1)
+    ref = orc.decompress(words, (n,), op)
+    d = gc.decode(torch.from_numpy(np.concatenate([words, np.zeros(2, np.uint64)]).view(np.int64)).cuda(), (n,),
+                  P(gc, op))
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy().view(np.uint32), ref.view(np.uint32))
