@@ -489,3 +489,11 @@ def test_fast1d_decode_arbitrary_streams(gc, orc, r):
                   P(gc, op))
     torch.cuda.synchronize()
     assert np.array_equal(d.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("params", [(64, 64, 20, -1074), (64, 64, 64, -100), (32, 32, 12, -1074), (32, 32, 64, -60)])
+def test_fixed1d_generic_coder(gc, orc, params):
+    """Whole-word fixed-rate 1-D blocks outside the lean coder's domain (kmin > 0 possible): generic coder and
+    generic decoder, vs the oracle."""
+    a = np.concatenate([orc.gen_normal(4 * 5000 + 3, 1e-3, 31, True), orc.gen_normal(4000, 1.0, 32, False)])
+    _check_vs_oracle(gc, orc, a, orc.expert(*params))

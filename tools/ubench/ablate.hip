@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../gcow_amd/csrc/gcow_kernels.hip"
+#include "legacy_variants.hip"
 
 namespace gcow {
 
