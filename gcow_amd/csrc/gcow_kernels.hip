@@ -734,6 +734,204 @@ __global__ __launch_bounds__(T) void k_encode_tiles(FieldDesc F, Params p, uint3
   }
 }
 
+// ------------------------------------------------------------------------------------------------ 1-D variable rate
+// Closed-form coder for variable-rate 1-D blocks (accuracy / precision / expert modes whose budget never truncates a
+// block: minbits <= 1, maxbits >= 160). Same structure as lean-4, with the plane range ending at kmin = 32 - prec:
+//   header (9) | empty planes 31 .. max(M0, kmin - 1) + 1 ('0' each) | group phase M0 .. max(T2, kmin), one plane
+//   per wave-uniform step through the 80-entry plane table (lanes past their own group phase emit verbatim nibbles,
+//   lanes past kmin emit nothing) | verbatim nibbles down to kmin from the 32-plane window.
+// Returns the block's bit length; with CODE the bits in c[0..2] (a block is at most 140 bits). special: Inf/NaN, or a
+// group phase longer than 16 planes or 64 bits -> generic coder.
+template <bool CODE>
+__device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uint16_t* tab, int minexp,
+                                                      uint32_t maxprec, uint64_t* c, bool& special)
+{
+  const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
+  const uint32_t a2 = __float_as_uint(f[2]) & 0x7fffffffu, a3 = __float_as_uint(f[3]) & 0x7fffffffu;
+  const uint32_t m = max(max(a0, a1), max(a2, a3));
+  special = m >= 0x7f800000u;
+  const uint32_t E = special ? 150u : (m >> 23);
+  const int emax = (int)max(E, 1u) - 126;  // frexp exponent of max|x|, clamped at -126
+  const int prec = min((int)maxprec, max(0, emax - minexp + 4));
+  if (CODE) c[0] = c[1] = c[2] = 0ull;
+  if (m == 0 || prec == 0) return 1u;  // one 0 bit
+  const int kmin = prec < 32 ? 32 - prec : 0;
+  const bool tiny = E < 29u;
+  const float s = __uint_as_float((283u - (tiny ? 150u : E)) << 23);
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = tiny ? (int32_t)0x80000000 : (int32_t)(f[i] * s);
+  fwd_lift(q[0], q[1], q[2], q[3]);
+  uint32_t u[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = ((uint32_t)q[i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+  const uint32_t o23 = u[2] | u[3];
+  const int M0 = 31 - (int)__builtin_clz(u[0] | u[1] | o23 | 1u);
+  const int T2 = o23 ? 31 - (int)__builtin_clz(o23) : 0;
+  const uint32_t pos0 = 9u + (uint32_t)(31 - max(M0, kmin - 1));  // header + empty planes
+  const int nplanes = max(M0 - kmin + 1, 0);                        // planes M0 .. kmin
+  const int jg = M0 - max(T2, kmin);                                 // last group-phase plane (window index)
+  const uint64_t Y = plane_window(u, (uint32_t)(31 - M0));
+  uint64_t g = 0;  // group-phase bits, relative to pos0
+  uint32_t glen = 0, n = 0;
+  int j = 0;
+#pragma unroll
+  for (; j < 16; j++) {
+    if (!__any(j <= jg)) break;
+    const uint32_t e = tab[(n << 4) | ((uint32_t)(Y >> (4 * j)) & 15u)];
+    const bool act = j < nplanes;
+    const uint32_t len = act ? (e >> 7) & 7u : 0u;
+    if (CODE) g |= (uint64_t)(act && glen < 64 ? (e & 127u) : 0u) << glen;
+    glen += len;
+    n = act ? e >> 10 : n;
+  }
+  special = special || jg >= 16 || glen > 64;
+  const int tplanes = max(nplanes - j, 0);  // verbatim planes after the group phase
+  const uint32_t len = pos0 + glen + 4u * (uint32_t)tplanes;
+  if (CODE) {
+    const uint64_t hdr = 2ull * E + 3ull;
+    c[0] = hdr | (pos0 < 64 ? g << pos0 : 0ull);
+    c[1] = pos0 ? g >> (64 - pos0) : 0ull;  // pos0 >= 9
+    if (tplanes > 0) {
+      // tail nibbles j .. nplanes-1 of the 32-plane window (Y, then planes M0-16 .. M0-31)
+      const uint64_t Y2 = nplanes > 16 ? plane_window(u, (uint32_t)min(47 - M0, 31)) : 0ull;
+      // j is the wave-uniform group-loop count, 1..16 (16 when another lane's group phase filled the window)
+      uint64_t t0 = j == 16 ? Y2 : (Y >> (4 * j)) | (Y2 << (64 - 4 * j));
+      uint64_t t1 = j == 16 ? 0ull : Y2 >> (4 * j);
+      const uint32_t tb = 4u * (uint32_t)tplanes;  // <= 128
+      if (tb < 64) { t0 &= (1ull << tb) - 1ull; t1 = 0; }
+      else if (tb < 128) t1 &= (1ull << (tb - 64)) - 1ull;
+      const uint32_t pt = pos0 + glen;  // in [9, 137]
+      if (pt < 64) {
+        c[0] |= t0 << pt;
+        c[1] |= (t0 >> (64 - pt)) | (t1 << pt);
+        c[2] |= t1 >> (64 - pt);
+      } else if (pt < 128) {
+        const uint32_t q2 = pt - 64;
+        c[1] |= t0 << q2;
+        c[2] |= (q2 ? t0 >> (64 - q2) : 0ull) | (t1 << q2);
+      } else {
+        c[2] |= t0 << (pt - 128);
+      }
+    }
+  }
+  return len;
+}
+
+// Variable-rate 1-D pass 1: per-range sums of block bit lengths (closed-form coder; generic for special blocks).
+template <int DT>
+__global__ __launch_bounds__(256) void k_count1d_var(FieldDesc F, Params p, uint32_t range, uint64_t* __restrict__ sums)
+{
+  __shared__ uint16_t tab[80];
+  __shared__ uint64_t red[4];
+  if (threadIdx.x < 80) tab[threadIdx.x] = plane_entry4(threadIdx.x);
+  __syncthreads();
+  const uint64_t b0 = (uint64_t)blockIdx.x * range;
+  const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
+  uint64_t acc = 0;
+  for (uint64_t t0 = b0; t0 < b1; t0 += 256) {  // wave-uniform trip count (the coder uses wave votes)
+    const uint64_t b = t0 + threadIdx.x;
+    float f[4] = {0, 0, 0, 0};
+    if (b < b1) gather_block<1, DT>(F, (uint32_t)b, f);
+    bool special;
+    uint32_t len = encode_block1d_var<false>(f, tab, p.minexp, p.maxprec, nullptr, special);
+    if (special && b < b1) {
+      CountWriter w;
+      len = encode_block<1>(w, f, p);
+    }
+    acc += b < b1 ? len : 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) sums[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// Variable-rate 1-D pass 2: k_encode_tiles with the closed-form coder; each lane ORs its <= 140-bit code into the
+// tile's LDS window with 64-bit LDS atomics.
+template <int DT>
+__global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uint32_t range,
+                                                      const uint64_t* __restrict__ rbase, uint32_t* __restrict__ out32,
+                                                      uint64_t* __restrict__ index, uint32_t index_shift)
+{
+  constexpr uint32_t T = 256;
+  __shared__ uint64_t lds64[(31 + T * 160 + 63) / 64 + 4];
+  __shared__ uint32_t scan_sh[T / 64];
+  __shared__ uint16_t tab[80];
+  uint32_t* lds = (uint32_t*)lds64;
+  const uint32_t tid = threadIdx.x;
+  if (tid < 80) tab[tid] = plane_entry4(tid);
+  const uint64_t b0 = (uint64_t)blockIdx.x * range;
+  const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
+  const bool final_range = b1 == F.nblocks;
+  uint64_t base = rbase[blockIdx.x];
+  const uint64_t first_word = base >> 5;
+  const bool first_shared = (base & 31) != 0;
+  uint32_t carry = 0;
+  __syncthreads();
+  for (uint64_t t0 = b0; t0 < b1; t0 += T) {
+    const uint64_t b = t0 + tid;
+    const bool valid = b < b1;
+    float f[4] = {0, 0, 0, 0};
+    if (valid) gather_block<1, DT>(F, (uint32_t)b, f);
+    uint64_t c[3];
+    bool special;
+    uint32_t len = encode_block1d_var<true>(f, tab, p.minexp, p.maxprec, c, special);
+    special = special && valid;
+    if (special) {
+      CountWriter cw;
+      len = encode_block<1>(cw, f, p);
+    }
+    len = valid ? len : 0u;
+    uint32_t tile_total;
+    const uint32_t excl = block_exclusive_scan<T>(len, &tile_total, scan_sh);
+    const uint32_t lbase = (uint32_t)(base & 31);
+    const uint32_t end_local = lbase + tile_total;
+    const uint32_t W = (end_local + 31) >> 5;
+    for (uint32_t j = tid; j < (W + 3) / 2; j += T) lds64[j] = 0ull;
+    __syncthreads();
+    if (tid == 0) lds[0] |= carry;
+    __syncthreads();
+    if (valid) {
+      const uint32_t o = lbase + excl;
+      if (special) {
+        LdsWriter w{lds, o, o + len};
+        encode_block<1>(w, f, p);
+      } else {
+        const uint32_t qw = o >> 6, sh = o & 63u;
+        const uint32_t nq = (sh + len + 63) >> 6;  // 1..4 qwords touched
+        atomicOr((unsigned long long*)&lds64[qw], (unsigned long long)(c[0] << sh));
+        if (nq > 1) atomicOr((unsigned long long*)&lds64[qw + 1],
+                             (unsigned long long)((sh ? c[0] >> (64 - sh) : 0ull) | (c[1] << sh)));
+        if (nq > 2) atomicOr((unsigned long long*)&lds64[qw + 2],
+                             (unsigned long long)((sh ? c[1] >> (64 - sh) : 0ull) | (c[2] << sh)));
+        if (nq > 3) atomicOr((unsigned long long*)&lds64[qw + 3], (unsigned long long)(c[2] >> (64 - sh)));
+      }
+      if (index && ((b & ((1ull << index_shift) - 1)) == 0)) index[b >> index_shift] = base + excl;
+    }
+    __syncthreads();
+    const bool last_tile = t0 + T >= b1;
+    const bool partial = (end_local & 31) != 0;
+    const uint32_t Wstore = (last_tile || !partial) ? W : (end_local >> 5);
+    const uint64_t gw0 = base >> 5;
+    for (uint32_t j = tid; j < Wstore; j += T) {
+      const uint64_t gw = gw0 + j;
+      const uint32_t v = lds[j];
+      const bool shared = (gw == first_word && first_shared) || (last_tile && partial && !final_range && j == W - 1);
+      if (shared) atomicOr(out32 + gw, v);
+      else out32[gw] = v;
+    }
+    if (last_tile && final_range && tid == 0) {
+      const uint64_t endw = (base + tile_total + 31) >> 5;
+      if (endw & 1) out32[endw] = 0u;
+    }
+    carry = (!last_tile && partial) ? lds[end_local >> 5] : 0u;
+    base += tile_total;
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ decode
 template <int D>
 __global__ __launch_bounds__(64) void k_decode(FieldDesc F, Params p, const uint64_t* __restrict__ in,
@@ -1213,8 +1411,14 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
     kern<<<plan.nranges, T, lds, st>>>(F, p, plan.range, nullptr, out32, index, index_shift);
     return hipGetLastError();
   }
-  k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
+  const bool var1d = D == 1 && T == 256 && p.minbits <= 1 && p.maxbits >= 160 && !getenv("GCOW_GENERIC_VAR");
+  if (var1d) k_count1d_var<DT><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
+  else k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   k_scan_ranges<<<1, 1024, 0, st>>>(ws_sums, plan.nranges, ws_base, d_total, out32);
+  if (var1d) {
+    k_encode1d_var<DT><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_base, out32, index, index_shift);
+    return hipGetLastError();
+  }
   auto kern = k_encode_tiles<D, DT, T, false>;
   if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   kern<<<plan.nranges, T, lds, st>>>(F, p, plan.range, ws_base, out32, index, index_shift);

@@ -497,3 +497,45 @@ def test_fixed1d_generic_coder(gc, orc, params):
     generic decoder, vs the oracle."""
     a = np.concatenate([orc.gen_normal(4 * 5000 + 3, 1e-3, 31, True), orc.gen_normal(4000, 1.0, 32, False)])
     _check_vs_oracle(gc, orc, a, orc.expert(*params))
+
+
+def _adversarial_1d(seed):
+    rng = np.random.default_rng(seed)
+    nb = 1 << 14
+    sign = np.where(rng.random((nb, 4)) < 0.5, -1.0, 1.0)
+    wide = sign * 2.0 ** rng.uniform(-60, 10, (nb, 4))
+    const = np.repeat(rng.standard_normal((nb // 4, 1)), 4, axis=1)
+    alt = np.repeat(rng.standard_normal((nb // 4, 1)), 4, axis=1) * np.array([1, -1, 1, -1])
+    pow2 = 2.0 ** rng.integers(-60, 30, (nb // 4, 4)) * np.where(rng.random((nb // 4, 4)) < 0.5, -1.0, 1.0)
+    ramp = np.cumsum(rng.standard_normal((nb // 4, 4)) * 1e-6, axis=1) + 1.0
+    tiny = rng.standard_normal((nb // 8, 4)) * 1e-38
+    return np.concatenate([wide, const, alt, pow2, ramp, tiny]).astype(np.float32).reshape(-1)
+
+
+@pytest.mark.parametrize("mode", ["acc1e-6", "acc1e-3", "acc1e-20", "acc1e-30", "prec32", "prec20", "prec5",
+                                  "expert_max", "expert_maxprec12"])
+def test_var1d_closed_form_coder(gc, orc, mode):
+    """1-D variable-rate blocks through the closed-form coder (long group phases, many planes, tiny / subnormal /
+    const / alternating blocks, partial last block), stream and decode vs the oracle, with a block index."""
+    a = np.concatenate([_adversarial_1d(3), orc.gen_normal((1 << 18) + 3, 1e-3, 77, True)])
+    op = {"acc1e-6": orc.accuracy(1e-6), "acc1e-3": orc.accuracy(1e-3), "acc1e-20": orc.accuracy(1e-20),
+          "acc1e-30": orc.accuracy(1e-30), "prec32": orc.precision(32), "prec20": orc.precision(20),
+          "prec5": orc.precision(5), "expert_max": orc.expert(1, 16658, 64, -1074),
+          "expert_maxprec12": orc.expert(1, 16658, 12, -30)}[mode]
+    _check_vs_oracle(gc, orc, a, op, index_stride=16)
+
+
+def test_c5_full_size_bf16_accuracy(gc, orc):
+    """BASELINE config 5 shape: 256 Mi bf16 values (exact widening), accuracy 1e-6, vs the threaded oracle."""
+    n = 256 * 1024 * 1024
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    gc.fill_normal(x, 1e-3, seed=0x67636F77, inject=True)
+    xb = x.to(torch.bfloat16)
+    del x
+    hb = xb.cpu().view(torch.int16).numpy().view(np.uint16)
+    op = orc.accuracy(1e-6)
+    w_ref, bits_ref = orc.compress(hb, op, threads=min(16, os.cpu_count() or 1))
+    e = gc.encode(xb, P(gc, op), index_stride=16)
+    torch.cuda.synchronize()
+    assert e.bits == bits_ref
+    assert np.array_equal(e.stream().cpu().numpy().view(np.uint64), w_ref)
