@@ -207,6 +207,24 @@ __device__ __forceinline__ typename PlaneType<B>::T get_plane(const uint32_t* u,
   return x;
 }
 
+// In-place 32 x 32 bit-matrix transpose, LSB-first: bit c of a[i] <-> bit i of a[c]. Five delta-swap stages
+// (16 swaps each); an involution, so the same call turns coefficient words into bit planes and back.
+__device__ __forceinline__ void transpose32(uint32_t* a)
+{
+#pragma unroll
+  for (int s = 16, st = 0; s > 0; s >>= 1, st++) {
+    const uint32_t m = s == 16 ? 0x0000FFFFu : s == 8 ? 0x00FF00FFu : s == 4 ? 0x0F0F0F0Fu : s == 2 ? 0x33333333u
+                                                                                                    : 0x55555555u;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+      if (i & s) continue;
+      const uint32_t t = ((a[i] >> s) ^ a[i + s]) & m;
+      a[i + s] ^= t;
+      a[i] ^= t << s;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ writers
 // A writer appends bits LSB-first; put(v, n) requires v < 2^n (n <= 64), skip(n) appends zeros.
 // Every writer truncates at its limit, which makes the untruncated coder below equal the budgeted one.
@@ -361,7 +379,9 @@ struct BitReader {
   }
 };
 
-// decode_ints (libzfp 0.5.5; sw/src/decode.c:141-183 with block size 4^d)
+// decode_ints (libzfp 0.5.5; sw/src/decode.c:141-183 with block size 4^d). The unary scan of each group test
+// (`for (; n < size - 1 && bits && (bits--, !read_bit()); n++)`) is done with one count-trailing-zeros of the next
+// 64 stream bits instead of bit by bit.
 template <int B>
 __device__ __forceinline__ uint32_t decode_ints(BitReader& r, uint32_t maxbits, uint32_t maxprec, uint32_t* u)
 {
@@ -371,14 +391,29 @@ __device__ __forceinline__ uint32_t decode_ints(BitReader& r, uint32_t maxbits, 
 #pragma unroll
   for (int i = 0; i < B; i++) u[i] = 0;
   for (int k = 31; bits && k >= kmin; --k) {
-    uint32_t m = n < bits ? n : bits;
+    const uint32_t m = n < bits ? n : bits;
     bits -= m;
     uint64_t x = r.get(m);
-    for (; n < (uint32_t)B && bits && (bits--, r.bit()); x += 1ull << n++)
-      for (; n < (uint32_t)B - 1 && bits && (bits--, !r.bit()); n++)
-        ;
+    while (n < (uint32_t)B && bits) {
+      bits--;
+      if (!r.bit()) break;  // negative group test
+      const uint32_t lim = min((uint32_t)B - 1 - n, bits);  // zeros the scan may read
+      const uint64_t w = r.peek64();
+      const uint32_t z = w ? (uint32_t)__builtin_ctzll(w) : 64u;
+      if (z < lim) {  // zeros, then the one-bit
+        r.pos += z + 1;
+        bits -= z + 1;
+        n += z;
+      } else {  // scan ran into the last coefficient or the budget: the one is implied
+        r.pos += lim;
+        bits -= lim;
+        n += lim;
+      }
+      x += 1ull << n;
+      n++;
+    }
 #pragma unroll
-    for (int i = 0; i < B; i++) u[i] += (uint32_t)((x >> i) & 1u) << k;
+    for (int i = 0; i < B; i++) u[i] |= (uint32_t)((x >> i) & 1u) << k;
   }
   return maxbits - bits;
 }

@@ -131,10 +131,15 @@ __device__ __forceinline__ void scatter_block(const FieldDesc& F, uint32_t b, co
         *(float4*)(out + base + (int64_t)y * F.s[1] + (int64_t)z * F.s[2]) = make_float4(g[0], g[1], g[2], g[3]);
       }
   } else {
-    for (uint32_t z = 0; z < nvz; z++)
-      for (uint32_t y = 0; y < nvy; y++)
-        for (uint32_t x = 0; x < nvx; x++)
-          out[base + (int64_t)x * F.s[0] + (int64_t)y * F.s[1] + (int64_t)z * F.s[2]] = f[16 * z + 4 * y + x];
+    // static trip counts with guards: a dynamically indexed f[] would live in scratch
+#pragma unroll
+    for (uint32_t z = 0; z < (D > 2 ? 4u : 1u); z++)
+#pragma unroll
+      for (uint32_t y = 0; y < (D > 1 ? 4u : 1u); y++)
+#pragma unroll
+        for (uint32_t x = 0; x < 4u; x++)
+          if (x < nvx && y < nvy && z < nvz)
+            out[base + (int64_t)x * F.s[0] + (int64_t)y * F.s[1] + (int64_t)z * F.s[2]] = f[16 * z + 4 * y + x];
   }
 }
 
