@@ -209,20 +209,25 @@ __device__ __forceinline__ typename PlaneType<B>::T get_plane(const uint32_t* u,
 
 // In-place 32 x 32 bit-matrix transpose, LSB-first: bit c of a[i] <-> bit i of a[c]. Five delta-swap stages
 // (16 swaps each); an involution, so the same call turns coefficient words into bit planes and back.
-__device__ __forceinline__ void transpose32(uint32_t* a)
+template <int S, uint32_t M>
+__device__ __forceinline__ void transpose32_stage(uint32_t* a)
 {
 #pragma unroll
-  for (int s = 16, st = 0; s > 0; s >>= 1, st++) {
-    const uint32_t m = s == 16 ? 0x0000FFFFu : s == 8 ? 0x00FF00FFu : s == 4 ? 0x0F0F0F0Fu : s == 2 ? 0x33333333u
-                                                                                                    : 0x55555555u;
-#pragma unroll
-    for (int i = 0; i < 32; i++) {
-      if (i & s) continue;
-      const uint32_t t = ((a[i] >> s) ^ a[i + s]) & m;
-      a[i + s] ^= t;
-      a[i] ^= t << s;
-    }
+  for (int i = 0; i < 32; i++) {
+    if (i & S) continue;
+    const uint32_t t = ((a[i] >> S) ^ a[i + S]) & M;
+    a[i + S] ^= t;
+    a[i] ^= t << S;
   }
+}
+
+__device__ __forceinline__ void transpose32(uint32_t* a)
+{
+  transpose32_stage<16, 0x0000FFFFu>(a);
+  transpose32_stage<8, 0x00FF00FFu>(a);
+  transpose32_stage<4, 0x0F0F0F0Fu>(a);
+  transpose32_stage<2, 0x33333333u>(a);
+  transpose32_stage<1, 0x55555555u>(a);
 }
 
 // ------------------------------------------------------------------------------------------------ writers
@@ -271,39 +276,69 @@ struct LdsWriter {
 // ------------------------------------------------------------------------------------------------ coder
 // encode_partial_bitplanes / encode_all_bitplanes (encode.c:279-408). Emits the untruncated plane codes until the
 // budget is consumed; returns min(untruncated bits, budget) = what the budgeted coder writes.
+// One bit plane of the embedded coder: n bits verbatim, then the group tests of the remainder.
+template <int B, class W>
+__device__ __forceinline__ void encode_plane(W& w, typename PlaneType<B>::T x, uint32_t budget, uint32_t& bits,
+                                             uint32_t& n)
+{
+  using PT = typename PlaneType<B>::T;
+  // step 2: first n bits verbatim
+  w.put((uint64_t)x & lowmask64(n), n);
+  bits += n;
+  PT r = n < (uint32_t)B ? (PT)(x >> n) : (PT)0;
+  // step 3: unary run-length (group test) code of the remainder
+  while (n < (uint32_t)B && bits < budget) {
+    if (r == 0) {  // negative group test: done with this plane
+      w.skip(1);
+      bits += 1;
+      break;
+    }
+    const uint32_t t = (B == 64) ? (uint32_t)__builtin_ctzll((uint64_t)r) : (uint32_t)__builtin_ctz((uint32_t)r);
+    if (n + t < (uint32_t)B - 1) {  // group '1', t zeros, the one-bit
+      w.put(1ull | (2ull << t), t + 2);
+      bits += t + 2;
+      n += t + 1;
+      r = (PT)(r >> (t + 1));
+    } else {  // the one-bit sits in the last position and is implied
+      w.put(1ull, 1);
+      w.skip(B - 1 - n);
+      bits += B - n;
+      n = B;
+    }
+  }
+}
+
+// Planes K, K-1, ..., 0 of a transposed 64-coefficient block with compile-time plane indices (a runtime index
+// into the plane registers would put them in scratch).
+template <int K, class W>
+__device__ __forceinline__ void encode_planes64(W& w, const uint32_t* t, int kmin, uint32_t budget, uint32_t& bits,
+                                                uint32_t& n)
+{
+  if constexpr (K >= 0) {
+    if (K < kmin || bits >= budget) return;
+    encode_plane<64>(w, (uint64_t)t[K] | ((uint64_t)t[32 + K] << 32), budget, bits, n);
+    encode_planes64<K - 1>(w, t, kmin, budget, bits, n);
+  }
+}
+
+// encode_partial_bitplanes / encode_all_bitplanes (encode.c:279-408). Emits the untruncated plane codes until the
+// budget is consumed; returns min(untruncated bits, budget) = what the budgeted coder writes. 64-coefficient blocks
+// form all 32 planes with two 32 x 32 bit transposes instead of 64 bit gathers per plane.
 template <int B, class W>
 __device__ __forceinline__ uint32_t encode_ints(W& w, const uint32_t* u, uint32_t budget, uint32_t maxprec)
 {
-  using PT = typename PlaneType<B>::T;
   const int kmin = maxprec < 32 ? 32 - (int)maxprec : 0;
   uint32_t bits = 0;
   uint32_t n = 0;
-  for (int k = 31; k >= kmin && bits < budget; --k) {
-    PT x = get_plane<B>(u, k);
-    // step 2: first n bits verbatim
-    w.put((uint64_t)x & lowmask64(n), n);
-    bits += n;
-    PT r = n < (uint32_t)B ? (PT)(x >> n) : (PT)0;
-    // step 3: unary run-length (group test) code of the remainder
-    while (n < (uint32_t)B && bits < budget) {
-      if (r == 0) {  // negative group test: done with this plane
-        w.skip(1);
-        bits += 1;
-        break;
-      }
-      uint32_t t = (B == 64) ? (uint32_t)__builtin_ctzll((uint64_t)r) : (uint32_t)__builtin_ctz((uint32_t)r);
-      if (n + t < (uint32_t)B - 1) {  // group '1', t zeros, the one-bit
-        w.put(1ull | (2ull << t), t + 2);
-        bits += t + 2;
-        n += t + 1;
-        r = (PT)(r >> (t + 1));
-      } else {  // the one-bit sits in the last position and is implied
-        w.put(1ull, 1);
-        w.skip(B - 1 - n);
-        bits += B - n;
-        n = B;
-      }
-    }
+  if constexpr (B == 64) {
+    uint32_t t[64];
+#pragma unroll
+    for (int i = 0; i < 64; i++) t[i] = u[i];
+    transpose32(t);
+    transpose32(t + 32);
+    encode_planes64<31>(w, t, kmin, budget, bits, n);
+  } else {
+    for (int k = 31; k >= kmin && bits < budget; --k) encode_plane<B>(w, get_plane<B>(u, k), budget, bits, n);
   }
   return bits < budget ? bits : budget;
 }
