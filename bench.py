@@ -34,8 +34,8 @@ N_VALUES = 256 * 1024 * 1024
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--rate", type=float, default=16.0)
     ap.add_argument("--values", type=int, default=N_VALUES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -213,7 +213,7 @@ def main():
             cpu = {"error": repr(ex)}
 
     if rank == 0:
-        kname = "k_encode_fixed1d_pipe"
+        kname = "k_encode_fixed1d_np"
         traffic = load_pmc_traffic(kname, workload)
         line = {
             "metric": "GiB/s device-resident fp32->ZFP encode, 256Mi-float bucket, 1/2/4/8 GPU",

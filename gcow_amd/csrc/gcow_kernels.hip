@@ -291,61 +291,7 @@ __device__ __forceinline__ uint64_t plane_window(const uint32_t* u, uint32_t sh)
   return transpose4x16(x);
 }
 
-// Lean-4 block. Two facts shorten the wave-uniform group-test loop of lean-3:
-//  * with three coefficients significant (n = 3) a plane's code is its nibble verbatim: the three known bits, then
-//    the group test for coefficient 3 -- which is that coefficient's bit, its own 1 being implied (encode.c:318-333);
-//    so the group phase ends at plane T2 = max(L2, L3), not at L3;
-//  * lanes whose group phase is over keep looking up plane pairs: rows n >= 3 of the pair table are verbatim, so the
-//    extra iterations emit tail nibbles and the loop needs no per-lane activity masks; the tail then starts at the
-//    same (wave-uniform) window nibble for every lane.
-template <uint32_t WB>
-__device__ __forceinline__ uint64_t encode_block1d_lean4(const float* f, const uint32_t* tab2, bool& special)
-{
-  const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
-  const uint32_t a2 = __float_as_uint(f[2]) & 0x7fffffffu, a3 = __float_as_uint(f[3]) & 0x7fffffffu;
-  const uint32_t m = max(max(a0, a1), max(a2, a3));
-  special = m >= 0x7f800000u;  // Inf or NaN present
-  const bool zero = m == 0;
-  const uint32_t E = special ? 150u : (m >> 23);
-  const bool tiny = E < 29u;
-  const float s = __uint_as_float((283u - (tiny ? 150u : E)) << 23);
-  int32_t q[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) q[i] = tiny ? (int32_t)0x80000000 : (int32_t)(f[i] * s);
-  fwd_lift(q[0], q[1], q[2], q[3]);
-  uint32_t u[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) u[i] = ((uint32_t)q[i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
-  uint64_t acc = 2ull * E + 3ull;
-  const uint32_t o23 = u[2] | u[3];
-  const int M0 = 31 - (int)__builtin_clz(u[0] | u[1] | o23 | 1u);
-  const int T2 = o23 ? 31 - (int)__builtin_clz(o23) : 0;  // group phase: planes M0 .. max(T2, 0)
-  uint32_t pos = 9 + (uint32_t)(31 - M0);
-  const uint64_t Y = plane_window(u, (uint32_t)(31 - M0));
-  const int jg = M0 - T2;
-  uint32_t n = 0;
-  int j = 0;
-#pragma unroll
-  for (; j < 16; j += 2) {
-    if (!__any(j <= jg)) break;
-    const uint32_t e = tab2[(n << 8) | ((uint32_t)(Y >> (4 * j)) & 255u)];
-    const uint32_t code = pos < WB ? (e & 0x3fffu) : 0u;  // 64-bit shifts wrap: nothing past the budget
-    acc |= (uint64_t)code << pos;
-    pos += (e >> 14) & 15u;
-    n = e >> 18;
-  }
-  special = special || (jg >= 16 && pos < WB);  // group phase runs past the 16-plane window (generic coder)
-  if (j < 16 && pos < WB) acc |= (Y >> (4 * j)) << pos;  // rest of the window, verbatim
-  const uint32_t p2 = pos + 4u * (uint32_t)(16 - j);        // where plane M0 - 16 lands
-  if (__any(p2 < WB && M0 >= 16)) {
-    const uint64_t Y2 = plane_window(u, (uint32_t)max(47 - M0, 0));  // planes M0 - 16 .. M0 - 31
-    if (p2 < WB && M0 >= 16) acc |= Y2 << p2;
-  }
-  acc = zero ? 0ull : acc;
-  return WB == 64 ? acc : (acc & ((1ull << WB) - 1ull));
-}
-
-// Compile-time plane-pair table (plane_entry4x2 as constexpr), copied to LDS by each workgroup.
+// Compile-time plane-pair table (two plane codes per entry), copied to LDS by each workgroup.
 struct PlaneTab2 {
   uint32_t v[1280];
 };
@@ -377,7 +323,11 @@ __host__ __device__ constexpr uint32_t plane_entry4_cx(uint32_t t)
   return code | (len << 7) | (n << 10);
 }
 
-__host__ __device__ constexpr PlaneTab2 make_plane_tab2()
+
+// ---- lean-5: the pair table re-packed so a lookup chains into the next with one and-or, a 32-bit group-code
+// accumulator for the first two pairs, and the all-INT_MIN ("tiny") block as a compile-time constant.
+// Entry: n' << 10 (= the next row's byte offset) | len << 13 | code << 17 (two 7-bit codes, len <= 14).
+__host__ __device__ constexpr PlaneTab2 make_plane_tab5()
 {
   PlaneTab2 T{};
   for (uint32_t t = 0; t < 1280; t++) {
@@ -386,12 +336,138 @@ __host__ __device__ constexpr PlaneTab2 make_plane_tab2()
     const uint32_t c1 = e1 & 127u, l1 = (e1 >> 7) & 7u, n1 = e1 >> 10;
     const uint32_t e2 = plane_entry4_cx((n1 << 4) | (b >> 4));
     const uint32_t c2 = e2 & 127u, l2 = (e2 >> 7) & 7u, n2 = e2 >> 10;
-    T.v[t] = (c1 | (c2 << l1)) | ((l1 + l2) << 14) | (n2 << 18);
+    T.v[t] = (n2 << 10) | ((l1 + l2) << 13) | ((c1 | (c2 << l1)) << 17);
   }
   return T;
 }
 
-__device__ const PlaneTab2 g_plane_tab2 = make_plane_tab2();
+__device__ const PlaneTab2 g_plane_tab5 = make_plane_tab5();
+
+// Embedded coder of one 4-coefficient block with kmin = 0 (encode.c:279-339 restated for compile-time use): the
+// first `budget` payload bits, LSB-first.
+__host__ __device__ constexpr uint64_t code4_cx(const uint32_t* u, int budget)
+{
+  uint64_t acc = 0;
+  int pos = 0, bits = budget;
+  uint32_t n = 0;
+  for (int k = 31; k >= 0 && bits > 0; --k) {
+    uint32_t x = 0;
+    for (int i = 0; i < 4; i++) x |= ((u[i] >> k) & 1u) << i;
+    const int m = (int)n < bits ? (int)n : bits;
+    acc |= (uint64_t)(x & ((1u << m) - 1u)) << pos;
+    pos += m;
+    x >>= m;
+    bits -= m;
+    while (bits > 0 && n < 4) {
+      bits--;
+      const uint32_t t = x != 0;
+      acc |= (uint64_t)t << pos++;
+      if (!t) break;
+      while (bits > 0 && n < 3) {
+        bits--;
+        const uint32_t b = x & 1u;
+        acc |= (uint64_t)b << pos++;
+        if (b) break;
+        x >>= 1;
+        n++;
+      }
+      x >>= 1;
+      n++;
+    }
+  }
+  return acc;
+}
+
+// Payload of a block whose every value casts to INT_MIN (scale 2^(30-e) = +inf, e <= -98; x86 cvttss2si,
+// encode.c:162-187): the lift (encode.c:212-225) and negabinary map (encode.c:263-275) of four INT_MIN.
+__host__ __device__ constexpr uint64_t tiny_payload_cx(int budget)
+{
+  auto asr = [](uint32_t v) { return (v >> 1) | (v & 0x80000000u); };
+  uint32_t x = 0x80000000u, y = x, z = x, w = x;
+  x += w; x = asr(x); w -= x;
+  z += y; z = asr(z); y -= z;
+  x += z; x = asr(x); z -= x;
+  w += y; w = asr(w); y -= w;
+  w += asr(y); y -= asr(w);
+  uint32_t u[4] = {(x + 0xaaaaaaaau) ^ 0xaaaaaaaau, (y + 0xaaaaaaaau) ^ 0xaaaaaaaau, (z + 0xaaaaaaaau) ^ 0xaaaaaaaau,
+                   (w + 0xaaaaaaaau) ^ 0xaaaaaaaau};
+  return code4_cx(u, budget);
+}
+
+// v_cvt_i32_f32 as an opaque instruction: saturating, NaN -> 0, never poison (lanes whose cast is out of range are
+// the tiny / special ones, whose result is replaced).
+__device__ __forceinline__ int32_t cvt_i32_hw(float x)
+{
+  int32_t r;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// Pair-table lookup chained on the previous entry's row (n' << 10 is already a byte offset).
+__device__ __forceinline__ uint32_t tab5_next(const uint32_t* tab, uint32_t e, uint32_t byte)
+{
+  return *(const uint32_t*)((const char*)tab + ((e & 0x1c00u) | (byte << 2)));
+}
+
+// Lean-5 block: same stream as lean-4 (and encode.c:457-495 for d = 1, fixed rate, kmin = 0).
+//  * tiny (all values cast to INT_MIN) and zero blocks are selected from constants at the end, so the cast needs
+//    no per-value range select;
+//  * pair 0 always starts at n = 0 and pair 1 is taken by ~92 % of waves: both accumulate in 32 bits (<= 28 code
+//    bits), one 64-bit shift places them; only pairs 2.. (about half the waves) use the budget-guarded 64-bit path.
+template <uint32_t WB>
+__device__ __forceinline__ uint64_t encode_block1d_lean5(const float* f, const uint32_t* tab, bool& special)
+{
+  const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
+  const uint32_t a2 = __float_as_uint(f[2]) & 0x7fffffffu, a3 = __float_as_uint(f[3]) & 0x7fffffffu;
+  const uint32_t m = max(max(a0, a1), max(a2, a3));
+  special = m >= 0x7f800000u;  // Inf or NaN present
+  const uint32_t E = m >> 23;
+  const float s = __uint_as_float((283u - E) << 23);  // 2^(30 - e); meaningless for tiny / special lanes
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = cvt_i32_hw(f[i] * s);
+  fwd_lift(q[0], q[1], q[2], q[3]);
+  uint32_t u[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = ((uint32_t)q[i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+  const uint32_t o23 = u[2] | u[3];
+  const uint32_t sh = __builtin_clz(u[0] | u[1] | o23 | 1u);  // 31 - M0
+  const int M0 = 31 - (int)sh;
+  const int jg = o23 ? (int)__builtin_clz(o23) - (int)sh : M0;  // group phase: window nibbles 0 .. jg
+  const uint64_t Y = plane_window(u, sh);
+  uint32_t pos = 9 + sh;
+  uint32_t e = tab[(uint32_t)Y & 255u];
+  uint32_t G = e >> 17, gl = (e >> 13) & 15u;
+  int j = 2;
+  if (__any(jg >= 2)) {
+    e = tab5_next(tab, e, ((uint32_t)Y >> 8) & 255u);
+    G |= (e >> 17) << gl;
+    gl += (e >> 13) & 15u;
+    j = 4;
+  }
+  uint64_t acc = (2ull * E + 3ull) | ((uint64_t)G << pos);
+  pos += gl;
+#pragma unroll
+  for (int jj = 4; jj < 16; jj += 2) {
+    if (j < jj || !__any(jj <= jg)) break;
+    e = tab5_next(tab, e, (uint32_t)(Y >> (4 * jj)) & 255u);
+    const uint32_t code = pos < WB ? (e >> 17) : 0u;  // 64-bit shifts wrap: nothing past the budget
+    acc |= (uint64_t)code << pos;
+    pos += (e >> 13) & 15u;
+    j = jj + 2;
+  }
+  special = special || (jg >= 16 && pos < WB);  // group phase runs past the 16-plane window (generic coder)
+  if (j < 16 && pos < WB) acc |= (Y >> (4 * j)) << pos;  // rest of the window, verbatim
+  const uint32_t p2 = pos + 4u * (uint32_t)(16 - j);      // where plane M0 - 16 lands
+  if (__any(p2 < WB && M0 >= 16)) {
+    const uint64_t Y2 = plane_window(u, (uint32_t)max(47 - M0, 0));  // planes M0 - 16 .. M0 - 31
+    if (p2 < WB && M0 >= 16) acc |= Y2 << p2;
+  }
+  constexpr uint64_t TINY = tiny_payload_cx((int)WB - 9) << 9;
+  const uint64_t tv = m ? (TINY | (2ull * E + 3ull)) : 0ull;
+  acc = E < 29u ? tv : acc;  // zero, subnormal and tiny-normal maxima: every value casts to INT_MIN (or is 0)
+  return WB == 64 ? acc : (acc & ((1ull << WB) - 1ull));
+}
 
 // ---- hand-counted memory pipeline for the persistent fixed-rate 1-D encoder
 // Loads and stores are raw buffer instructions issued from inline asm, so the compiler's waitcnt pass does not see
@@ -468,7 +544,7 @@ __global__ __launch_bounds__(256) void k_encode_fixed1d_pipe(const void* __restr
 {
   __shared__ uint32_t tab2[1280];
 #pragma unroll
-  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab5.v[t];
   __syncthreads();
   constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;  // input bytes per block
   const pipe_v4i rin = buf_rsrc(in, nfull * IB), rout = buf_rsrc(out, nfull * (WB / 8));
@@ -488,7 +564,7 @@ __global__ __launch_bounds__(256) void k_encode_fixed1d_pipe(const void* __restr
       float f[4];
       PipeRow<DT>::unpack(r[k], f);
       bool special;
-      uint64_t w = encode_block1d_lean4<WB>(f, tab2, special);
+      uint64_t w = encode_block1d_lean5<WB>(f, tab2, special);
       if (special) {
         RegWriter64 rw{0ull, 0u};
         encode_block<1>(rw, f, p);
@@ -503,6 +579,42 @@ __global__ __launch_bounds__(256) void k_encode_fixed1d_pipe(const void* __restr
         return;
       }
     }
+  }
+}
+
+// One-shot (non-persistent) fixed-rate 1-D encoder: each lane codes U blocks 256 apart inside its workgroup's chunk
+// of 256 U blocks. All U loads are issued first (before the LDS table fill), then each block waits for its own load
+// only: with U loads followed by k stores outstanding, load k has landed once at most U - 1 operations remain
+// (vmcnt counts loads and stores together, in issue order). Out-of-range lanes read zeros and their stores are
+// dropped by the buffer range check, so control flow stays wave-uniform. Measured against the persistent grid-stride
+// pipeline above, the one-shot shape streams HBM like a plain copy kernel.
+template <int DT, uint32_t WB, int U>
+__global__ __launch_bounds__(256) void k_encode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
+                                                           void* __restrict__ out)
+{
+  __shared__ uint32_t tab[1280];
+  constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;  // input bytes per block
+  const pipe_v4i rin = buf_rsrc(in, nfull * IB), rout = buf_rsrc(out, nfull * (WB / 8));
+  const uint32_t b0 = blockIdx.x * (256u * U) + threadIdx.x;
+  typename PipeRow<DT>::T r[U];
+#pragma unroll
+  for (int k = 0; k < U; k++) r[k] = PipeRow<DT>::load((b0 + 256u * k) * IB, rin);
+#pragma unroll
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab[t] = g_plane_tab5.v[t];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    pipe_wait<U - 1>(r[k]);
+    float f[4];
+    PipeRow<DT>::unpack(r[k], f);
+    bool special;
+    uint64_t w = encode_block1d_lean5<WB>(f, tab, special);
+    if (special) {
+      RegWriter64 rw{0ull, 0u};
+      encode_block<1>(rw, f, p);
+      w = WB == 64 ? rw.acc : (rw.acc & ((1ull << WB) - 1ull));
+    }
+    pipe_store<WB>((b0 + 256u * k) * (WB / 8), rout, w);
   }
 }
 
@@ -528,40 +640,6 @@ __global__ __launch_bounds__(256) void k_encode_fixed1d_generic(const void* __re
     const uint32_t b = b0 + 256u * j;
     if (b < nfull) {
       const uint64_t w = encode_block1d_fixed<WB>(f[j], p, tab);
-      if constexpr (WB == 64) ((uint64_t*)out)[b] = w;
-      else ((uint32_t*)out)[b] = (uint32_t)w;
-    }
-  }
-}
-
-// Fixed-rate 1-D encoder over the full 4-value blocks [0, nfull); U blocks per lane, loads issued first.
-template <int DT, uint32_t WB, int VARIANT>
-__global__ __launch_bounds__(256) void k_encode_fixed1d(const void* __restrict__ in, uint32_t nfull, Params p,
-                                                        void* __restrict__ out)
-{
-  __shared__ uint16_t tab[80];
-  if (threadIdx.x < 80) tab[threadIdx.x] = plane_entry4(threadIdx.x);
-  __syncthreads();
-  constexpr int U = 2;
-  const uint32_t b0 = blockIdx.x * (256u * U) + threadIdx.x;
-  float f[U][4];
-#pragma unroll
-  for (int j = 0; j < U; j++) {
-    const uint32_t b = b0 + 256u * j;
-    if (b < nfull) load_row4<DT>(in, 4ll * b, f[j]);
-  }
-#pragma unroll
-  for (int j = 0; j < U; j++) {
-    const uint32_t b = b0 + 256u * j;
-    if (b < nfull) {
-      uint64_t w;
-      if constexpr (VARIANT == 2) {
-        bool special;
-        w = encode_block1d_lean<WB>(f[j], tab, special);
-        if (special) w = encode_block1d_fixed<WB>(f[j], p, tab);
-      } else {
-        w = encode_block1d_fixed<WB, VARIANT>(f[j], p, tab);
-      }
       if constexpr (WB == 64) ((uint64_t*)out)[b] = w;
       else ((uint32_t*)out)[b] = (uint32_t)w;
     }
@@ -1143,6 +1221,41 @@ __global__ __launch_bounds__(256) void k_decode_fixed1d_pipe(const void* __restr
   }
 }
 
+// One-shot fixed-rate 1-D decoder (the shape of k_encode_fixed1d_np): each lane decodes U blocks 256 apart inside
+// its workgroup's chunk; the U word loads are issued before the table fill, and block k waits for its own word only
+// (U loads then k stores outstanding: vmcnt(U - 1)).
+template <uint32_t WB, int U>
+__global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
+                                                           float* __restrict__ out, uint64_t base_bits)
+{
+  __shared__ uint16_t dtab[5 * 8 * 128];
+  constexpr uint32_t WBYTES = WB / 8;
+  const pipe_v4i rin = buf_rsrc((const char*)in + base_bits / 8, nfull * WBYTES);
+  const __amdgpu_buffer_rsrc_t rout_b = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(nfull * 16u), 0x00020000);
+  const uint32_t b0 = blockIdx.x * (256u * U) + threadIdx.x;
+  typename PipeWord<WB>::T r[U];
+#pragma unroll
+  for (int k = 0; k < U; k++) r[k] = PipeWord<WB>::load((b0 + 256u * k) * WBYTES, rin);
+  for (uint32_t t = threadIdx.x; t < 5 * 8 * 128 / 2; t += 256)  // 10 KiB, copied as dwords
+    ((uint32_t*)dtab)[t] = ((const uint32_t*)g_dec_tab1.v)[t];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    pipe_wait<U - 1>(r[k]);
+    const uint32_t b = b0 + 256u * k;
+    float f[4];
+    bool special;
+    decode_block1d_fast<WB>(PipeWord<WB>::get(r[k]), dtab, f, special);
+    if (special && b < nfull) {
+      BitReader rd{(const uint64_t*)in, base_bits + (uint64_t)b * WB};
+      decode_block<1>(rd, p, f);
+    }
+    pipe_v4u v;
+    v.x = __float_as_uint(f[0]); v.y = __float_as_uint(f[1]); v.z = __float_as_uint(f[2]); v.w = __float_as_uint(f[3]);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rout_b, (int)(b * 16u), 0, 2);  // see k_decode_fixed1d_pipe
+  }
+}
+
 // the partial last block of a 1-D field (generic decoder, one lane)
 __global__ void k_decode_tail1d(FieldDesc F, Params p, const uint64_t* __restrict__ in, uint64_t base_bits,
                                 uint32_t b)
@@ -1352,9 +1465,20 @@ static int fixed1d_variant()
 {
   if (g_fixed1d_variant < 0) {
     const char* e = getenv("GCOW_FIXED1D_VARIANT");
-    g_fixed1d_variant = e ? atoi(e) : 9;  // 1 = generic coder (A/B and parity bisection)
+    g_fixed1d_variant = e ? atoi(e) : 8;  // 8/12/16 = one-shot lean-5 with U blocks per lane; 5 = persistent
+                                             // grid-stride lean-5, 1 = generic coder (A/B, parity bisection)
   }
   return g_fixed1d_variant;
+}
+
+static int decode1d_variant()
+{
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("GCOW_DECODE1D_VARIANT");
+    v = e ? atoi(e) : 16;  // 8 / 16 = one-shot with U blocks per lane, 0 = persistent pipeline
+  }
+  return v;
 }
 
 static int fixed1d_wgs_per_cu(int dflt = 32)
@@ -1378,11 +1502,16 @@ static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, vo
       constexpr uint32_t CH = 1u << 27;
       constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;
       const uint32_t wgs = (uint32_t)fixed1d_wgs_per_cu(12);
+      const int var = fixed1d_variant();
       for (uint32_t c0 = 0; c0 < nfull; c0 += CH) {
         const uint32_t nc = min(CH, nfull - c0);
         const uint32_t g = min((nc + 255) / 256, 256u * wgs);
-        k_encode_fixed1d_pipe<DT, WB, 3><<<g, 256, 0, st>>>((const char*)in + (size_t)c0 * IB, nc, p,
-                                                            (char*)out + (size_t)c0 * (WB / 8));
+        const void* ic = (const char*)in + (size_t)c0 * IB;
+        void* oc = (char*)out + (size_t)c0 * (WB / 8);
+        if (var == 16) k_encode_fixed1d_np<DT, WB, 16><<<(nc + 4095) / 4096, 256, 0, st>>>(ic, nc, p, oc);
+        else if (var == 8) k_encode_fixed1d_np<DT, WB, 8><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
+        else if (var == 12) k_encode_fixed1d_np<DT, WB, 12><<<(nc + 3071) / 3072, 256, 0, st>>>(ic, nc, p, oc);
+        else k_encode_fixed1d_pipe<DT, WB, 3><<<g, 256, 0, st>>>(ic, nc, p, oc);
       }
     }
   }
@@ -1473,8 +1602,17 @@ hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint
     const uint32_t g = min((nc + 255) / 256, 256u * wgs);
     float* out = (float*)F.data + (size_t)c0 * 4;
     const uint64_t bb = base_bits + (uint64_t)c0 * p.maxbits;
-    if (p.maxbits == 64) k_decode_fixed1d_pipe<64, 3><<<g, 256, 0, S(stream)>>>(in, nc, p, out, bb);
-    else k_decode_fixed1d_pipe<32, 3><<<g, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+    const int var = decode1d_variant();
+    if (var == 0) {  // persistent grid-stride pipeline (A/B)
+      if (p.maxbits == 64) k_decode_fixed1d_pipe<64, 3><<<g, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+      else k_decode_fixed1d_pipe<32, 3><<<g, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+    } else if (var == 8) {
+      if (p.maxbits == 64) k_decode_fixed1d_np<64, 8><<<(nc + 2047) / 2048, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+      else k_decode_fixed1d_np<32, 8><<<(nc + 2047) / 2048, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+    } else {
+      if (p.maxbits == 64) k_decode_fixed1d_np<64, 16><<<(nc + 4095) / 4096, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+      else k_decode_fixed1d_np<32, 16><<<(nc + 4095) / 4096, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+    }
   }
   if (F.n[0] % 4) k_decode_tail1d<<<1, 1, 0, S(stream)>>>(F, p, in, base_bits, nfull);
   return hipGetLastError();

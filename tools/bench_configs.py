@@ -23,10 +23,15 @@ sys.path.insert(0, ROOT)
 from gcow_amd import codec  # noqa: E402
 
 
-def timeit(fn, reps=10, rounds=3):
+def timeit(fn, reps=20, rounds=5, settle_s=0.2):
+    """Median per-call time; the first `settle_s` seconds of back-to-back calls are untimed (MI355X clocks dip for
+    ~5-10 ms after a burst starts and recover over ~50 ms)."""
     st = torch.cuda.current_stream()
-    fn()
-    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < settle_s:
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
     ts = []
     for _ in range(rounds):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -609,14 +609,76 @@ __global__ __launch_bounds__(256) void k_asm(const void* __restrict__ in, uint32
   }
 }
 
+
+// non-persistent lean-5: each lane codes U blocks (256 apart inside its workgroup's chunk), all loads issued first
+template <int U>
+__global__ __launch_bounds__(256) void k_np5(const void* __restrict__ in, uint32_t nfull, Params p, void* __restrict__ out)
+{
+  __shared__ uint32_t tab[1280];
+  const abl_v4i rin = abl_rsrc(in, nfull * 16u), rout = abl_rsrc(out, nfull * 8u);
+  const uint32_t b0 = blockIdx.x * (256u * U) + threadIdx.x;
+  abl_v4f r[U];
+#pragma unroll
+  for (int k = 0; k < U; k++) r[k] = abl_load((b0 + 256u * k) * 16u, rin);
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab[t] = g_plane_tab5.v[t];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    abl_wait<U - 1>(r[k]);
+    float f[4] = {r[k].x, r[k].y, r[k].z, r[k].w};
+    bool sp;
+    uint64_t w = encode_block1d_lean5<64>(f, tab, sp);
+    if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, f, p); w = rw.acc; }
+    abl_store((b0 + 256u * k) * 8u, rout, w);
+  }
+}
+
+// persistent lean-5 over contiguous per-workgroup chunks (stride 256 blocks) instead of a grid stride
+template <int NB>
+__global__ __launch_bounds__(256) void k_chunk5(const void* __restrict__ in, uint32_t nfull, Params p, void* __restrict__ out)
+{
+  __shared__ uint32_t tab[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab[t] = g_plane_tab5.v[t];
+  __syncthreads();
+  const uint32_t per = ((nfull + gridDim.x - 1) / gridDim.x + 255u) & ~255u;
+  const uint32_t lo = blockIdx.x * per, hi = min(nfull, lo + per);
+  const abl_v4i rin = abl_rsrc(in, hi * 16u), rout = abl_rsrc(out, hi * 8u);
+  uint32_t b = lo + threadIdx.x;
+  uint32_t bw = lo;
+  if (bw >= hi) return;
+  abl_v4f r[NB];
+#pragma unroll
+  for (int d = 0; d < NB; d++) r[d] = abl_load((b + d * 256u) * 16u, rin);
+#pragma unroll
+  for (int d = 0; d < NB; d++) abl_wait<0>(r[d]);
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      abl_wait<2 * (NB - 1)>(r[k]);
+      float f[4] = {r[k].x, r[k].y, r[k].z, r[k].w};
+      bool sp;
+      uint64_t w = encode_block1d_lean5<64>(f, tab, sp);
+      if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, f, p); w = rw.acc; }
+      abl_store(b * 8u, rout, w);
+      r[k] = abl_load((b + NB * 256u) * 16u, rin);
+      b += 256u;
+      bw += 256u;
+      if (bw >= hi) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+      }
+    }
+  }
+}
+
 // pure compute floor: each lane loads NB blocks once and re-encodes them for the wave's whole trip count
 // (same number of encodes as the real kernel, no per-iteration memory traffic), one store per lane at the end
-template <int NB>
+template <int NB, int CODER = 3>
 __global__ __launch_bounds__(256) void k_cfloor(const void* __restrict__ in, uint32_t nfull, Params p,
                                                  uint64_t* __restrict__ out)
 {
   __shared__ uint32_t tab2[1280];
-  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab2.v[t];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = CODER == 5 ? g_plane_tab5.v[t] : g_plane_tab2.v[t];
   __syncthreads();
   const uint32_t stride = gridDim.x * 256u;
   uint32_t b = blockIdx.x * 256u + threadIdx.x;
@@ -630,7 +692,8 @@ __global__ __launch_bounds__(256) void k_cfloor(const void* __restrict__ in, uin
 #pragma unroll
     for (int k = 0; k < NB; k++) {
       bool sp;
-      uint64_t w = encode_block1d_lean3<64>(r[k], tab2, sp);
+      uint64_t w = CODER == 5 ? encode_block1d_lean5<64>(r[k], tab2, sp)
+                   : CODER == 4 ? encode_block1d_lean4<64>(r[k], tab2, sp) : encode_block1d_lean3<64>(r[k], tab2, sp);
       if (sp) { RegWriter64 rw{0ull, 0u}; encode_block<1>(rw, r[k], p); w = rw.acc; }
       accx ^= w;
       r[k][0] = __uint_as_float(__float_as_uint(r[k][0]) ^ (uint32_t)(w & 1));  // keep the loop honest
@@ -710,6 +773,16 @@ extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, i
     case 51: gcow::k_encode_fixed1d_pipe<gcow::DT_F32, 64, 3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 52: gcow::k_encode_fixed1d_pipe<gcow::DT_F32, 64, 2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 53: gcow::k_encode_fixed1d_pipe<gcow::DT_F32, 64, 4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 54: gcow::k_cfloor<3, 4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 55: gcow::k_cfloor<3, 5><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
+    case 56: gcow::k_encode_fixed1d_pipe<gcow::DT_F32, 64, 3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 57: gcow::k_encode_fixed1d_pipe<gcow::DT_F32, 64, 2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 58: gcow::k_encode_fixed1d_pipe<gcow::DT_F32, 64, 4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 59: gcow::k_np5<2><<<(nfull + 511) / 512, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 60: gcow::k_np5<4><<<(nfull + 1023) / 1024, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 61: gcow::k_np5<8><<<(nfull + 2047) / 2048, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 62: gcow::k_chunk5<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 63: gcow::k_chunk5<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 9: gcow::k_floor1<false><<<(nfull + 255) / 256, 256, 0, st>>>((const float4*)in, nfull, (uint2*)out); break;
   }
   return (int)hipGetLastError();

@@ -3,6 +3,79 @@
 // lean-4 coder (gcow_amd/csrc/gcow_kernels.hip). Included by ablate.hip after gcow_kernels.hip.
 namespace gcow {
 
+// ---- lean-4 coder and its pair table (the product default before the lean-5 coder)
+__host__ __device__ constexpr PlaneTab2 make_plane_tab2()
+{
+  PlaneTab2 T{};
+  for (uint32_t t = 0; t < 1280; t++) {
+    const uint32_t n = t >> 8, b = t & 255u;
+    const uint32_t e1 = plane_entry4_cx((n << 4) | (b & 15u));
+    const uint32_t c1 = e1 & 127u, l1 = (e1 >> 7) & 7u, n1 = e1 >> 10;
+    const uint32_t e2 = plane_entry4_cx((n1 << 4) | (b >> 4));
+    const uint32_t c2 = e2 & 127u, l2 = (e2 >> 7) & 7u, n2 = e2 >> 10;
+    T.v[t] = (c1 | (c2 << l1)) | ((l1 + l2) << 14) | (n2 << 18);
+  }
+  return T;
+}
+
+__device__ const PlaneTab2 g_plane_tab2 = make_plane_tab2();
+
+// Lean-4 block. Two facts shorten the wave-uniform group-test loop of lean-3:
+//  * with three coefficients significant (n = 3) a plane's code is its nibble verbatim: the three known bits, then
+//    the group test for coefficient 3 -- which is that coefficient's bit, its own 1 being implied (encode.c:318-333);
+//    so the group phase ends at plane T2 = max(L2, L3), not at L3;
+//  * lanes whose group phase is over keep looking up plane pairs: rows n >= 3 of the pair table are verbatim, so the
+//    extra iterations emit tail nibbles and the loop needs no per-lane activity masks; the tail then starts at the
+//    same (wave-uniform) window nibble for every lane.
+template <uint32_t WB>
+__device__ __forceinline__ uint64_t encode_block1d_lean4(const float* f, const uint32_t* tab2, bool& special)
+{
+  const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
+  const uint32_t a2 = __float_as_uint(f[2]) & 0x7fffffffu, a3 = __float_as_uint(f[3]) & 0x7fffffffu;
+  const uint32_t m = max(max(a0, a1), max(a2, a3));
+  special = m >= 0x7f800000u;  // Inf or NaN present
+  const bool zero = m == 0;
+  const uint32_t E = special ? 150u : (m >> 23);
+  const bool tiny = E < 29u;
+  const float s = __uint_as_float((283u - (tiny ? 150u : E)) << 23);
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = tiny ? (int32_t)0x80000000 : (int32_t)(f[i] * s);
+  fwd_lift(q[0], q[1], q[2], q[3]);
+  uint32_t u[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] = ((uint32_t)q[i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+  uint64_t acc = 2ull * E + 3ull;
+  const uint32_t o23 = u[2] | u[3];
+  const int M0 = 31 - (int)__builtin_clz(u[0] | u[1] | o23 | 1u);
+  const int T2 = o23 ? 31 - (int)__builtin_clz(o23) : 0;  // group phase: planes M0 .. max(T2, 0)
+  uint32_t pos = 9 + (uint32_t)(31 - M0);
+  const uint64_t Y = plane_window(u, (uint32_t)(31 - M0));
+  const int jg = M0 - T2;
+  uint32_t n = 0;
+  int j = 0;
+#pragma unroll
+  for (; j < 16; j += 2) {
+    if (!__any(j <= jg)) break;
+    const uint32_t e = tab2[(n << 8) | ((uint32_t)(Y >> (4 * j)) & 255u)];
+    const uint32_t code = pos < WB ? (e & 0x3fffu) : 0u;  // 64-bit shifts wrap: nothing past the budget
+    acc |= (uint64_t)code << pos;
+    pos += (e >> 14) & 15u;
+    n = e >> 18;
+  }
+  special = special || (jg >= 16 && pos < WB);  // group phase runs past the 16-plane window (generic coder)
+  if (j < 16 && pos < WB) acc |= (Y >> (4 * j)) << pos;  // rest of the window, verbatim
+  const uint32_t p2 = pos + 4u * (uint32_t)(16 - j);        // where plane M0 - 16 lands
+  if (__any(p2 < WB && M0 >= 16)) {
+    const uint64_t Y2 = plane_window(u, (uint32_t)max(47 - M0, 0));  // planes M0 - 16 .. M0 - 31
+    if (p2 < WB && M0 >= 16) acc |= Y2 << p2;
+  }
+  acc = zero ? 0ull : acc;
+  return WB == 64 ? acc : (acc & ((1ull << WB) - 1ull));
+}
+
+
+
 // Lean 1-D fixed-rate block for parameters where every nonzero block has prec >= 32 (kmin = 0; the fixed-rate
 // default maxprec 64 / minexp -1074). "Normal" blocks (biased exponent of max|x| in [29, 254], no NaN/Inf) take a
 // straight path: the scale 2^(30 - emax) is finite and |x * scale| < 2^30, so the x86 INT_MIN corner cannot occur
