@@ -168,7 +168,7 @@ gcow_status encode_impl(const zfp_input* field, const gcow_params* p, void* d_ou
   const gcow::TilePlan pl = make_plan(F, *p);
   uint64_t *sums = nullptr, *base = nullptr;
   if (!pl.fixed) {
-    const size_t need = (2 * (size_t)pl.nranges + 1) * 8;
+    const size_t need = gcow_encode_workspace_bytes(field, p);
     if (!d_ws || ws_bytes < need) return fail(GCOW_ERR_INVALID, "workspace smaller than gcow_encode_workspace_bytes()");
     sums = (uint64_t*)d_ws;
     base = sums + pl.nranges;
@@ -680,7 +680,8 @@ size_t gcow_encode_workspace_bytes(const zfp_input* field, const gcow_params* p)
   gcow::FieldDesc F;
   if (make_field(field, F, false) || !p || p->minbits == p->maxbits) return 0;
   const gcow::TilePlan pl = make_plan(F, *p);
-  return (2 * (size_t)pl.nranges + 1) * 8;
+  const size_t two_pass = (2 * (size_t)pl.nranges + 1) * 8;
+  return F.dims == 1 ? std::max(two_pass, gcow::var1d_sp_workspace(F.nblocks)) : two_pass;
 }
 
 size_t gcow_index_entries(const zfp_input* field, uint32_t index_stride)

@@ -1015,6 +1015,164 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
   }
 }
 
+// ------------------------------------------------------------------------------------------------ 1-D variable rate,
+// single pass (decoupled look-back)
+// One workgroup per tile of 256 U consecutive blocks, tiles handed out in launch order by an atomic counter (so every
+// predecessor of a tile is resident or done). Each lane codes U consecutive blocks with the closed-form coder; the
+// tile's codes are assembled in LDS at tile-relative bit offsets; the tile total is published at once and one wave
+// looks back over the predecessors' published totals for the tile's global bit offset; the LDS words are then stored
+// shifted by that offset mod 32. The two words a tile shares with its neighbours go to a side array that
+// k_var_fixup merges. The input is read once (the two-pass form reads it twice and walks its tiles in series).
+// Descriptor: bits 62-63 status (0 empty, 1 tile total, 2 inclusive prefix), bits 0-61 value, written and read as one
+// 8-byte agent-scope atomic, so the value travels with its flag (cdna_hip_programming.md Guideline 16, form R2).
+constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1ull;
+
+template <int DT, int U>
+__global__ __launch_bounds__(256) void k_encode1d_var_sp(FieldDesc F, Params p, uint64_t* desc, uint32_t* ctr,
+                                                         uint32_t* __restrict__ fix, uint32_t ntiles,
+                                                         uint32_t* __restrict__ out32, uint64_t* __restrict__ d_total,
+                                                         uint64_t* __restrict__ index, uint32_t index_shift)
+{
+  constexpr uint32_t T = 256, TB = T * U;
+  constexpr uint32_t LW = (TB * 160 + 31) / 32 + 2;  // worst-case tile bits (a block is at most 140) + shift slack
+  __shared__ uint64_t lds64[(LW + 1) / 2];
+  __shared__ uint32_t scan_sh[T / 64];
+  __shared__ uint16_t tab[80];
+  __shared__ uint32_t s_tile;
+  __shared__ uint64_t s_prefix;
+  uint32_t* lds = (uint32_t*)lds64;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) s_tile = atomicAdd(ctr, 1u);
+  if (tid < 80) tab[tid] = plane_entry4(tid);
+  for (uint32_t j = tid; j < (LW + 1) / 2; j += T) lds64[j] = 0ull;
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint64_t nb = F.nblocks;
+  const uint64_t bl = (uint64_t)tile * TB + (uint64_t)tid * U;  // the lane's first block
+  float f[U][4];
+  if (bl + U <= nb && 4 * (bl + U) <= F.n[0]) {
+#pragma unroll
+    for (int k = 0; k < U; k++) load_row4<DT>(F.data, (int64_t)(4 * (bl + k)), f[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      f[k][0] = f[k][1] = f[k][2] = f[k][3] = 0.0f;
+      if (bl + k < nb) load_block1d<DT>(F.data, F.n[0], (uint32_t)(bl + k), f[k]);
+    }
+  }
+  uint64_t c[U][3];
+  uint32_t len[U];
+  bool sp[U];
+  uint32_t lsum = 0;
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    len[k] = encode_block1d_var<true>(f[k], tab, p.minexp, p.maxprec, c[k], sp[k]);
+    const bool valid = bl + k < nb;
+    sp[k] = sp[k] && valid;
+    if (sp[k]) {
+      CountWriter cw;
+      len[k] = encode_block<1>(cw, f[k], p);
+    }
+    len[k] = valid ? len[k] : 0u;
+    lsum += len[k];
+  }
+  uint32_t agg;
+  const uint32_t excl = block_exclusive_scan<T>(lsum, &agg, scan_sh);
+  if (tid == 0)
+    __hip_atomic_store(desc + tile, (tile ? LB_AGG : LB_INC) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // codes into LDS at tile-relative bit offsets (64-bit LDS atomics: neighbouring lanes share qwords)
+  uint32_t o = excl;
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    if (len[k]) {
+      if (sp[k]) {
+        LdsWriter w{lds, o, o + len[k]};
+        encode_block<1>(w, f[k], p);
+      } else {
+        const uint32_t qw = o >> 6, sh = o & 63u;
+        const uint32_t nq = (sh + len[k] + 63) >> 6;  // 1..4 qwords touched
+        atomicOr((unsigned long long*)&lds64[qw], (unsigned long long)(c[k][0] << sh));
+        if (nq > 1) atomicOr((unsigned long long*)&lds64[qw + 1],
+                             (unsigned long long)((sh ? c[k][0] >> (64 - sh) : 0ull) | (c[k][1] << sh)));
+        if (nq > 2) atomicOr((unsigned long long*)&lds64[qw + 2],
+                             (unsigned long long)((sh ? c[k][1] >> (64 - sh) : 0ull) | (c[k][2] << sh)));
+        if (nq > 3) atomicOr((unsigned long long*)&lds64[qw + 3], (unsigned long long)(c[k][2] >> (64 - sh)));
+      }
+    }
+    o += len[k];
+  }
+  // decoupled look-back: wave 0 reads 64 predecessor descriptors per step, nearest first; it stops at the nearest
+  // inclusive prefix, summing the tile totals in between, and waits while any descriptor before that one is empty
+  if (tid < 64) {
+    uint64_t prefix = 0;
+    if (tile) {
+      int64_t t = (int64_t)tile - 1;
+      uint32_t spins = 0;
+      for (;;) {
+        const int64_t i = t - (int64_t)tid;
+        const uint64_t v = i >= 0 ? __hip_atomic_load(desc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : LB_INC;
+        const uint64_t inc = __ballot((v >> 62) == 2u);
+        const uint64_t emp = __ballot((v >> 62) == 0u);
+        const uint32_t fi = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+        const uint64_t upto = fi >= 63 ? ~0ull : ((2ull << fi) - 1ull);
+        if (emp & upto) {
+          if (++spins > (1u << 26)) break;  // bounded spin (predecessors are resident, so never expected)
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        unsigned long long s = tid <= fi ? (v & LB_VAL) : 0ull;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        prefix += s;
+        if (fi < 64) break;
+        t -= 64;
+      }
+    }
+    if (tid == 0) {
+      if (tile) __hip_atomic_store(desc + tile, LB_INC | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_prefix = prefix;
+    }
+  }
+  __syncthreads();
+  const uint64_t base = s_prefix;
+  const uint32_t lb = (uint32_t)(base & 31u);
+  const uint32_t W = (lb + agg + 31) >> 5;
+  const bool last = tile == ntiles - 1;
+  const bool tailp = ((lb + agg) & 31u) != 0;
+  const uint64_t gw0 = base >> 5;
+  for (uint32_t j = tid; j < W; j += T) {
+    const uint32_t v = lb ? ((lds[j] << lb) | (j ? lds[j - 1] >> (32 - lb) : 0u)) : lds[j];
+    if (j == 0 && lb) fix[2 * tile] = v;                           // shared with the previous tile
+    else if (j == W - 1 && tailp && !last) fix[2 * tile + 1] = v;  // shared with the next tile
+    else out32[gw0 + j] = v;
+  }
+  if (index) {
+    uint64_t oo = base + excl;
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const uint64_t b = bl + k;
+      if (b < nb && (b & ((1ull << index_shift) - 1)) == 0) index[b >> index_shift] = oo;
+      oo += len[k];
+    }
+  }
+  if (last && tid == 0) {
+    const uint64_t E = base + agg;
+    if (d_total) *d_total = E;
+    const uint64_t ew = (E + 31) >> 5;
+    if (ew & 1) out32[ew] = 0u;  // stream_flush: zero-pad to a 64-bit boundary
+  }
+}
+
+// The word holding tile t's first bit (when not 32-bit aligned) = tile t-1's tail bits | tile t's head bits.
+__global__ void k_var_fixup(const uint64_t* __restrict__ desc, const uint32_t* __restrict__ fix, uint32_t ntiles,
+                            uint32_t* __restrict__ out32)
+{
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x + 1u;
+  if (t >= ntiles) return;
+  const uint64_t s = desc[t - 1] & LB_VAL;  // inclusive prefix of tile t-1 = first bit of tile t
+  if (s & 31u) out32[s >> 5] = fix[2 * (t - 1) + 1] | fix[2 * t];
+}
+
 // ------------------------------------------------------------------------------------------------ decode
 template <int D>
 __global__ __launch_bounds__(64) void k_decode(FieldDesc F, Params p, const uint64_t* __restrict__ in,
@@ -1546,6 +1704,20 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
     return hipGetLastError();
   }
   const bool var1d = D == 1 && T == 256 && p.minbits <= 1 && p.maxbits >= 160 && !getenv("GCOW_GENERIC_VAR");
+  if constexpr (D == 1 && T == 256) {
+    if (var1d && F.vec && !getenv("GCOW_VAR1D_2PASS")) {  // single pass; ws_sums is the workspace start
+      const uint32_t ntiles = var1d_sp_tiles(F.nblocks);
+      uint64_t* desc = ws_sums;
+      uint32_t* ctr = (uint32_t*)(desc + ((ntiles + 1) & ~1u));
+      uint32_t* fix = ctr + 4;
+      hipError_t e = hipMemsetAsync(desc, 0, (size_t)((ntiles + 1) & ~1u) * 8 + 16, st);
+      if (e != hipSuccess) return e;
+      k_encode1d_var_sp<DT, 2><<<ntiles, 256, 0, st>>>(F, p, desc, ctr, fix, ntiles, out32, d_total, index,
+                                                       index_shift);
+      if (ntiles > 1) k_var_fixup<<<(ntiles - 1 + 255) / 256, 256, 0, st>>>(desc, fix, ntiles, out32);
+      return hipGetLastError();
+    }
+  }
   if (var1d) k_count1d_var<DT><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   else k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   k_scan_ranges<<<1, 1024, 0, st>>>(ws_sums, plan.nranges, ws_base, d_total, out32);

@@ -539,3 +539,22 @@ def test_c5_full_size_bf16_accuracy(gc, orc):
     torch.cuda.synchronize()
     assert e.bits == bits_ref
     assert np.array_equal(e.stream().cpu().numpy().view(np.uint64), w_ref)
+
+
+@pytest.mark.parametrize("nblocks", [1, 511, 512, 513, 1024, 5000, 100003])
+@pytest.mark.parametrize("mode", ["acc1e-3", "sparse"])
+def test_var1d_single_pass_tiles(gc, orc, nblocks, mode):
+    """Single-pass variable-rate 1-D encoder (512-block tiles, decoupled look-back) across tile boundaries: partial
+    last tile and block, exact multiples, mostly-zero tiles (1-bit blocks: tile boundaries on 32-bit words), stream +
+    block index + decode vs the oracle."""
+    n = 4 * nblocks - (1 if nblocks > 1 else 0)
+    if mode == "acc1e-3":
+        a = orc.gen_normal(n, 1e-3, 1000 + nblocks, True)
+        op = orc.accuracy(1e-3)
+    else:
+        a = np.zeros(n, np.float32)
+        rng = np.random.default_rng(nblocks)
+        hit = rng.integers(0, n, max(1, n // 300))
+        a[hit] = rng.standard_normal(hit.size).astype(np.float32)
+        op = orc.accuracy(1e-6)
+    _check_vs_oracle(gc, orc, a, op, index_stride=16)

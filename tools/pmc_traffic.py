@@ -4,7 +4,9 @@ from separate --pmc FETCH_SIZE and --pmc WRITE_SIZE passes, corrected per MI355X
 FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced
 streaming read, so it is doubled; WRITE_SIZE is exact for 16-B/lane streaming stores (8-B stores: uncalibrated).
 
-usage: pmc_traffic.py <kernel-substring> <workload> <kt_dir> <fetch_dir> <write_dir> <out_prefix>
+usage: pmc_traffic.py <kernel-substring> <workload> <kt_dir> <fetch_dir> <write_dir> <out_prefix> [timed_steps]
+With timed_steps K, the kernel trace's last K launches (bench.py's timed region, after its warmup) are averaged as
+well: the stats CSV averages every launch, warmup included.
 """
 import csv
 import json
@@ -19,6 +21,7 @@ def per_launch(path, kernel, counter):
 
 def main():
     kernel, workload, kt, fetch, write, out = sys.argv[1:7]
+    timed = int(sys.argv[7]) if len(sys.argv) > 7 else 0
     stats = [r for r in csv.DictReader(open(kt + "/kt_kernel_stats.csv"))]
     f_kib, nf = per_launch(fetch + "/pmc_counter_collection.csv", kernel, "FETCH_SIZE")
     w_kib, nw = per_launch(write + "/pmc_counter_collection.csv", kernel, "WRITE_SIZE")
@@ -36,6 +39,12 @@ def main():
         "correction": "read = 2 x FETCH_SIZE KiB (gfx950 wide-stream halving), write = WRITE_SIZE KiB",
         "launches_sampled": [nf, nw],
     }
+    if timed:
+        rows = [r for r in csv.DictReader(open(kt + "/kt_kernel_trace.csv")) if kernel in r["Kernel_Name"]]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows][-timed:]
+        d["timed_region_launches"] = len(dur)
+        d["timed_region_avg_duration_ns"] = sum(dur) / len(dur) if dur else None
     json.dump(d, open(out + "_pmc_traffic.json", "w"), indent=1)
     with open(out + "_kernel_stats.csv", "w") as fo:
         fo.write(open(kt + "/kt_kernel_stats.csv").read())
