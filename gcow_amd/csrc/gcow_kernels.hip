@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "codec_device.h"
 #include "kernels.h"
@@ -1027,8 +1028,59 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
 // 8-byte agent-scope atomic, so the value travels with its flag (cdna_hip_programming.md Guideline 16, form R2).
 constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1ull;
 
+// U consecutive 4-value blocks starting at block bl (zeros past the end; padded gather for a partial last block)
 template <int DT, int U>
+__device__ __forceinline__ void load_blocks1d(const FieldDesc& F, uint64_t bl, float (&f)[U][4])
+{
+  const uint64_t nb = F.nblocks;
+  if (bl + U <= nb && 4 * (bl + U) <= F.n[0]) {
+#pragma unroll
+    for (int k = 0; k < U; k++) load_row4<DT>(F.data, (int64_t)(4 * (bl + k)), f[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      f[k][0] = f[k][1] = f[k][2] = f[k][3] = 0.0f;
+      if (bl + k < nb) load_block1d<DT>(F.data, F.n[0], (uint32_t)(bl + k), f[k]);
+    }
+  }
+}
+
+// Variable-rate 1-D tile totals (one workgroup per tile of 256 U blocks): the count pass of the scan form.
+template <int DT, int U>
+__global__ __launch_bounds__(256) void k_count1d_var_tiles(FieldDesc F, Params p, uint64_t* __restrict__ sums)
+{
+  __shared__ uint16_t tab[80];
+  __shared__ uint32_t red[4];
+  const uint32_t tid = threadIdx.x;
+  if (tid < 80) tab[tid] = plane_entry4(tid);
+  __syncthreads();
+  const uint64_t bl = (uint64_t)blockIdx.x * (256u * U) + (uint64_t)tid * U;
+  float f[U][4];
+  load_blocks1d<DT, U>(F, bl, f);
+  uint32_t lsum = 0;
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    bool sp;
+    uint32_t len = encode_block1d_var<false>(f[k], tab, p.minexp, p.maxprec, nullptr, sp);
+    const bool valid = bl + k < F.nblocks;
+    if (sp && valid) {
+      CountWriter cw;
+      len = encode_block<1>(cw, f[k], p);
+    }
+    lsum += valid ? len : 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = lsum;
+  __syncthreads();
+  if (tid == 0) sums[blockIdx.x] = (uint64_t)red[0] + red[1] + red[2] + red[3];
+}
+
+// LOOKBACK: tile numbers from the atomic counter and the tile offset from the decoupled look-back over desc;
+// otherwise tile = blockIdx.x and its offset is rbase[tile] (exclusive scan of k_count1d_var_tiles' totals).
+template <int DT, int U, bool LOOKBACK>
 __global__ __launch_bounds__(256) void k_encode1d_var_sp(FieldDesc F, Params p, uint64_t* desc, uint32_t* ctr,
+                                                         const uint64_t* __restrict__ rbase,
                                                          uint32_t* __restrict__ fix, uint32_t ntiles,
                                                          uint32_t* __restrict__ out32, uint64_t* __restrict__ d_total,
                                                          uint64_t* __restrict__ index, uint32_t index_shift)
@@ -1042,24 +1094,15 @@ __global__ __launch_bounds__(256) void k_encode1d_var_sp(FieldDesc F, Params p, 
   __shared__ uint64_t s_prefix;
   uint32_t* lds = (uint32_t*)lds64;
   const uint32_t tid = threadIdx.x;
-  if (tid == 0) s_tile = atomicAdd(ctr, 1u);
+  if (LOOKBACK && tid == 0) s_tile = atomicAdd(ctr, 1u);
   if (tid < 80) tab[tid] = plane_entry4(tid);
   for (uint32_t j = tid; j < (LW + 1) / 2; j += T) lds64[j] = 0ull;
   __syncthreads();
-  const uint32_t tile = s_tile;
+  const uint32_t tile = LOOKBACK ? s_tile : blockIdx.x;
   const uint64_t nb = F.nblocks;
   const uint64_t bl = (uint64_t)tile * TB + (uint64_t)tid * U;  // the lane's first block
   float f[U][4];
-  if (bl + U <= nb && 4 * (bl + U) <= F.n[0]) {
-#pragma unroll
-    for (int k = 0; k < U; k++) load_row4<DT>(F.data, (int64_t)(4 * (bl + k)), f[k]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < U; k++) {
-      f[k][0] = f[k][1] = f[k][2] = f[k][3] = 0.0f;
-      if (bl + k < nb) load_block1d<DT>(F.data, F.n[0], (uint32_t)(bl + k), f[k]);
-    }
-  }
+  load_blocks1d<DT, U>(F, bl, f);
   uint64_t c[U][3];
   uint32_t len[U];
   bool sp[U];
@@ -1078,7 +1121,7 @@ __global__ __launch_bounds__(256) void k_encode1d_var_sp(FieldDesc F, Params p, 
   }
   uint32_t agg;
   const uint32_t excl = block_exclusive_scan<T>(lsum, &agg, scan_sh);
-  if (tid == 0)
+  if (LOOKBACK && tid == 0)
     __hip_atomic_store(desc + tile, (tile ? LB_AGG : LB_INC) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // codes into LDS at tile-relative bit offsets (64-bit LDS atomics: neighbouring lanes share qwords)
   uint32_t o = excl;
@@ -1103,7 +1146,9 @@ __global__ __launch_bounds__(256) void k_encode1d_var_sp(FieldDesc F, Params p, 
   }
   // decoupled look-back: wave 0 reads 64 predecessor descriptors per step, nearest first; it stops at the nearest
   // inclusive prefix, summing the tile totals in between, and waits while any descriptor before that one is empty
-  if (tid < 64) {
+  if (!LOOKBACK) {
+    if (tid == 0) s_prefix = rbase[tile];
+  } else if (tid < 64) {
     uint64_t prefix = 0;
     if (tile) {
       int64_t t = (int64_t)tile - 1;
@@ -1164,12 +1209,13 @@ __global__ __launch_bounds__(256) void k_encode1d_var_sp(FieldDesc F, Params p, 
 }
 
 // The word holding tile t's first bit (when not 32-bit aligned) = tile t-1's tail bits | tile t's head bits.
-__global__ void k_var_fixup(const uint64_t* __restrict__ desc, const uint32_t* __restrict__ fix, uint32_t ntiles,
-                            uint32_t* __restrict__ out32)
+// starts: look-back descriptors (flagged: inclusive prefix of tile t-1) or the scanned tile offsets (tile t's start).
+__global__ void k_var_fixup(const uint64_t* __restrict__ starts, int flagged, const uint32_t* __restrict__ fix,
+                            uint32_t ntiles, uint32_t* __restrict__ out32)
 {
   const uint32_t t = blockIdx.x * 256u + threadIdx.x + 1u;
   if (t >= ntiles) return;
-  const uint64_t s = desc[t - 1] & LB_VAL;  // inclusive prefix of tile t-1 = first bit of tile t
+  const uint64_t s = flagged ? (starts[t - 1] & LB_VAL) : starts[t];  // first bit of tile t
   if (s & 31u) out32[s >> 5] = fix[2 * (t - 1) + 1] | fix[2 * t];
 }
 
@@ -1705,16 +1751,29 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
   }
   const bool var1d = D == 1 && T == 256 && p.minbits <= 1 && p.maxbits >= 160 && !getenv("GCOW_GENERIC_VAR");
   if constexpr (D == 1 && T == 256) {
-    if (var1d && F.vec && !getenv("GCOW_VAR1D_2PASS")) {  // single pass; ws_sums is the workspace start
+    const char* vm = getenv("GCOW_VAR1D_MODE");  // "2pass" (range form), "lookback" (single pass); default scan
+    const bool lookback = vm && !strcmp(vm, "lookback");
+    if (var1d && F.vec && !(vm && !strcmp(vm, "2pass"))) {  // tile forms; ws_sums is the workspace start
       const uint32_t ntiles = var1d_sp_tiles(F.nblocks);
-      uint64_t* desc = ws_sums;
-      uint32_t* ctr = (uint32_t*)(desc + ((ntiles + 1) & ~1u));
-      uint32_t* fix = ctr + 4;
-      hipError_t e = hipMemsetAsync(desc, 0, (size_t)((ntiles + 1) & ~1u) * 8 + 16, st);
-      if (e != hipSuccess) return e;
-      k_encode1d_var_sp<DT, 2><<<ntiles, 256, 0, st>>>(F, p, desc, ctr, fix, ntiles, out32, d_total, index,
-                                                       index_shift);
-      if (ntiles > 1) k_var_fixup<<<(ntiles - 1 + 255) / 256, 256, 0, st>>>(desc, fix, ntiles, out32);
+      if (lookback) {
+        uint64_t* desc = ws_sums;
+        uint32_t* ctr = (uint32_t*)(desc + ((ntiles + 1) & ~1u));
+        uint32_t* fix = ctr + 4;
+        hipError_t e = hipMemsetAsync(desc, 0, (size_t)((ntiles + 1) & ~1u) * 8 + 16, st);
+        if (e != hipSuccess) return e;
+        k_encode1d_var_sp<DT, 2, true><<<ntiles, 256, 0, st>>>(F, p, desc, ctr, nullptr, fix, ntiles, out32, d_total,
+                                                               index, index_shift);
+        if (ntiles > 1) k_var_fixup<<<(ntiles - 1 + 255) / 256, 256, 0, st>>>(desc, 1, fix, ntiles, out32);
+      } else {
+        uint64_t* sums = ws_sums;
+        uint64_t* base = sums + ntiles;
+        uint32_t* fix = (uint32_t*)(base + ntiles + 1);
+        k_count1d_var_tiles<DT, 2><<<ntiles, 256, 0, st>>>(F, p, sums);
+        k_scan_ranges<<<1, 1024, 0, st>>>(sums, ntiles, base, d_total, out32);
+        k_encode1d_var_sp<DT, 2, false><<<ntiles, 256, 0, st>>>(F, p, nullptr, nullptr, base, fix, ntiles, out32,
+                                                                d_total, index, index_shift);
+        if (ntiles > 1) k_var_fixup<<<(ntiles - 1 + 255) / 256, 256, 0, st>>>(base, 0, fix, ntiles, out32);
+      }
       return hipGetLastError();
     }
   }

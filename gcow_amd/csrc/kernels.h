@@ -29,10 +29,10 @@ struct TilePlan {
   bool fixed;          // minbits == maxbits: offsets are b * maxbits
 };
 
-// Single-pass variable-rate 1-D encoder (k_encode1d_var_sp): tiles of 512 blocks; workspace = tile descriptors
-// (padded to an even count) + a 16-B counter block + two boundary words per tile.
+// Tile forms of the variable-rate 1-D encoder (k_count1d_var_tiles / k_encode1d_var_sp): tiles of 512 blocks;
+// workspace = tile totals + scanned offsets (+1) + two boundary words per tile (the look-back form needs less).
 inline uint32_t var1d_sp_tiles(uint64_t nblocks) { return (uint32_t)((nblocks + 511) / 512); }
-inline size_t var1d_sp_workspace(uint64_t nblocks) { return 16 * (size_t)var1d_sp_tiles(nblocks) + 32; }
+inline size_t var1d_sp_workspace(uint64_t nblocks) { return 24 * (size_t)var1d_sp_tiles(nblocks) + 32; }
 
 hipError_t launch_encode_fixed1d(const void* in, int dtype, uint64_t nvals, uint32_t nblocks, const Params& p,
                                  void* out, void* stream);
