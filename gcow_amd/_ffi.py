@@ -102,6 +102,7 @@ def load():
         "gcow_encode_workspace_bytes": (sz, [pi, pp]),
         "gcow_index_entries": (sz, [pi, u32]),
         "gcow_encode_device": (i32, [pi, pp, vp, sz, vp, vp, sz, vp, u32, vp]),
+        "gcow_encode_device_append": (i32, [pi, pp, vp, sz, vp, vp, vp, sz, vp, u32, vp]),
         "gcow_decode_device": (i32, [pi, pp, vp, sz, vp, u32, vp]),
         "gcow_stitch_device": (i32, [vp, u64, vp, u64, vp]),
         "gcow_header_bits": (C.c_uint, [pp]),

@@ -287,3 +287,112 @@ def decompress_numpy(words: torch.Tensor, out: torch.Tensor | None = None, strea
     check(load().gcow_decode_device_at(C.byref(f), C.byref(p), w.data_ptr(), w.numel() * 8, hb, None, 0,
                                        _stream_ptr(stream)), "gcow_decode_device_at")
     return out
+
+
+# ------------------------------------------------------------------------------------------- chunked / host paths
+def encode_append(x: torch.Tensor, params: GcowParams, words: torch.Tensor, d_base: torch.Tensor,
+                  d_total: torch.Tensor, ws: torch.Tensor | None = None, index: torch.Tensor | None = None,
+                  index_stride: int = 0, stream=None):
+    """Append a variable-rate encode of device tensor x to the stream in `words` whose first d_base[0] bits are
+    already written (gcow_encode_device_append); d_total[0] receives the new end. d_base / d_total are int64 device
+    tensors (one element each); chunks appended this way equal one encode of their concatenation."""
+    L = load()
+    f = field_of(x)
+    need = L.gcow_encode_workspace_bytes(C.byref(f), C.byref(params))
+    if ws is None or ws.numel() * 8 < need:
+        ws = torch.empty(max(need // 8, 1), dtype=torch.int64, device=x.device)
+    st = L.gcow_encode_device_append(C.byref(f), C.byref(params), words.data_ptr(), words.numel() * 8,
+                                     d_base.data_ptr(), d_total.data_ptr(), ws.data_ptr(), ws.numel() * 8,
+                                     index.data_ptr() if index is not None else None, index_stride,
+                                     _stream_ptr(stream))
+    check(st, "gcow_encode_device_append")
+    return ws
+
+
+class HostEncoder:
+    """Encode a 1-D bucket that starts and ends in pinned host memory (the gradient bucket headed for the NIC,
+    BASELINE config 5), with the PCIe copies overlapped: the bucket is cut into `chunks` block-aligned chunks and
+    chunk i+1's H2D copy, chunk i's encode and chunk i-1's D2H copy run on three streams at once. Variable rate
+    appends each chunk at the device-side end of the previous one (gcow_encode_device_append); fixed rate writes
+    chunk i at its known word offset. Only whole 64-bit words that no later chunk touches are copied back early.
+    The result is byte-identical to one device encode of the whole bucket."""
+
+    def __init__(self, n: int, dtype, params: GcowParams, chunks: int = 8, device=None):
+        self.n, self.dtype, self.params = int(n), dtype, params
+        self.device = torch.device(device or "cuda")
+        self.fixed = is_fixed(params)
+        nb = (self.n + 3) // 4
+        per = max(16, ((nb + chunks - 1) // chunks + 15) // 16 * 16)  # 16-block multiples: 64-bit aligned chunks
+        self.bounds = []
+        b = 0
+        while b < nb:
+            e = min(b + per, nb)
+            self.bounds.append((4 * b, min(4 * e, self.n)))
+            b = e
+        self.L = load()
+        self.cap = max_output_bytes((self.n,), params, dtype)
+        self.words = torch.zeros((self.cap + 7) // 8 + 2, dtype=torch.int64, device=self.device)
+        self.bufs = [torch.empty(4 * per, dtype=dtype, device=self.device) for _ in range(2)]
+        f = field_of_shape((4 * per,), dtype)
+        need = self.L.gcow_encode_workspace_bytes(C.byref(f), C.byref(params))
+        self.ws = torch.empty(max(need // 8, 1), dtype=torch.int64, device=self.device)
+        k = len(self.bounds)
+        self.d_bits = torch.zeros(k + 1, dtype=torch.int64, device=self.device)
+        self.h_bits = torch.zeros(k + 1, dtype=torch.int64).pin_memory()
+        self.s_h2d, self.s_enc, self.s_d2h = (torch.cuda.Stream(self.device) for _ in range(3))
+
+    def __call__(self, h_in: torch.Tensor, h_out: torch.Tensor) -> int:
+        """h_in: pinned host 1-D tensor (n values); h_out: pinned host int64 tensor with room for the stream.
+        Returns the stream's bit count; h_out[:ceil(bits / 64)] holds the flushed stream."""
+        if h_in.numel() != self.n or h_in.dtype != self.dtype or h_in.is_cuda:
+            raise GcowError("HostEncoder built for %d %s host values" % (self.n, self.dtype))
+        p = self.params
+        k = len(self.bounds)
+        ev_h2d = [torch.cuda.Event() for _ in range(k)]
+        ev_enc = [torch.cuda.Event() for _ in range(k)]
+        done = 0  # words already copied back
+
+        def copy_back(end_word, after):
+            nonlocal done
+            if end_word > done:
+                self.s_d2h.wait_event(after)
+                with torch.cuda.stream(self.s_d2h):
+                    h_out[done:end_word].copy_(self.words[done:end_word], non_blocking=True)
+                done = end_word
+
+        for i, (lo, hi) in enumerate(self.bounds):
+            buf = self.bufs[i % 2]
+            if i >= 2:
+                self.s_h2d.wait_event(ev_enc[i - 2])  # the buffer's previous chunk is encoded
+            with torch.cuda.stream(self.s_h2d):
+                buf[: hi - lo].copy_(h_in[lo:hi], non_blocking=True)
+                ev_h2d[i].record(self.s_h2d)
+            self.s_enc.wait_event(ev_h2d[i])
+            x = buf[: hi - lo]
+            if self.fixed:
+                f = field_of(x)
+                off = (lo // 4) * p.maxbits // 8
+                check(self.L.gcow_encode_device(C.byref(f), C.byref(p), self.words.data_ptr() + off,
+                                                self.cap - off, None, None, 0, None, 0,
+                                                _stream_ptr(self.s_enc)), "gcow_encode_device")
+            else:
+                encode_append(x, p, self.words, self.d_bits[i:i + 1], self.d_bits[i + 1:i + 2], self.ws,
+                              stream=self.s_enc)
+                with torch.cuda.stream(self.s_enc):
+                    self.h_bits[i + 1:i + 2].copy_(self.d_bits[i + 1:i + 2], non_blocking=True)
+            ev_enc[i].record(self.s_enc)
+            if i >= 1:  # chunk i-1's complete words (chunk i only ORs into the word its first bit falls in)
+                if self.fixed:
+                    end = (self.bounds[i - 1][1] + 3) // 4 * p.maxbits
+                else:
+                    ev_enc[i - 1].synchronize()
+                    end = int(self.h_bits[i])
+                copy_back(end // 64, ev_enc[i - 1])
+        if self.fixed:
+            bits = ((self.n + 3) // 4) * p.maxbits
+        else:
+            ev_enc[k - 1].synchronize()
+            bits = int(self.h_bits[k])
+        copy_back((bits + 63) // 64, ev_enc[k - 1])
+        self.s_d2h.synchronize()
+        return bits

@@ -138,7 +138,7 @@ bool fast1d_ok(const gcow::FieldDesc& F, const gcow_params& p, const uint64_t* d
 
 gcow_status encode_impl(const zfp_input* field, const gcow_params* p, void* d_out, size_t out_capacity,
                         uint64_t* d_total_bits, void* d_ws, size_t ws_bytes, uint64_t* d_index,
-                        uint32_t index_stride, void* stream)
+                        uint32_t index_stride, void* stream, const uint64_t* d_base = nullptr)
 {
   gcow::FieldDesc F;
   gcow_status st = make_field(field, F, false);
@@ -153,8 +153,14 @@ gcow_status encode_impl(const zfp_input* field, const gcow_params* p, void* d_ou
       return fail(GCOW_ERR_INVALID, "index_stride must be a power of two in [1, 256]");
     while ((1u << shift) < index_stride) shift++;
   }
+  if (d_base && p->minbits == p->maxbits)
+    return fail(GCOW_ERR_UNSUPPORTED, "append with a device base offset is for variable-rate streams (fixed rate: "
+                                      "offset the output pointer by nblocks * maxbits / 8 on the host)");
   if (F.nblocks == 0) {
-    if (d_total_bits) GCOW_HIP(gcow::launch_set_u64(d_total_bits, 0, stream));
+    if (d_total_bits) {
+      if (d_base) GCOW_HIP(hipMemcpyAsync(d_total_bits, d_base, 8, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+      else GCOW_HIP(gcow::launch_set_u64(d_total_bits, 0, stream));
+    }
     return GCOW_OK;
   }
   const gcow::Params pp = P(*p);
@@ -174,7 +180,7 @@ gcow_status encode_impl(const zfp_input* field, const gcow_params* p, void* d_ou
     base = sums + pl.nranges;
   }
   GCOW_HIP(gcow::launch_encode_tiles(F, pp, pl, (uint32_t*)d_out, sums, base, pl.fixed ? nullptr : d_total_bits,
-                                     d_index, shift, stream));
+                                     d_index, shift, d_base, stream));
   if (pl.fixed && d_total_bits)
     GCOW_HIP(gcow::launch_set_u64(d_total_bits, (uint64_t)F.nblocks * p->maxbits, stream));
   return GCOW_OK;
@@ -680,8 +686,7 @@ size_t gcow_encode_workspace_bytes(const zfp_input* field, const gcow_params* p)
   gcow::FieldDesc F;
   if (make_field(field, F, false) || !p || p->minbits == p->maxbits) return 0;
   const gcow::TilePlan pl = make_plan(F, *p);
-  const size_t two_pass = (2 * (size_t)pl.nranges + 1) * 8;
-  return F.dims == 1 ? std::max(two_pass, gcow::var1d_sp_workspace(F.nblocks)) : two_pass;
+  return (2 * (size_t)pl.nranges + 1) * 8;
 }
 
 size_t gcow_index_entries(const zfp_input* field, uint32_t index_stride)
@@ -697,6 +702,16 @@ gcow_status gcow_encode_device(const zfp_input* field, const gcow_params* p, voi
 {
   return encode_impl(field, p, d_out, out_capacity, d_total_bits, d_workspace, workspace_bytes, d_index, index_stride,
                      hip_stream);
+}
+
+gcow_status gcow_encode_device_append(const zfp_input* field, const gcow_params* p, void* d_out, size_t out_capacity,
+                                      const uint64_t* d_base_bits, uint64_t* d_total_bits, void* d_workspace,
+                                      size_t workspace_bytes, uint64_t* d_index, uint32_t index_stride,
+                                      void* hip_stream)
+{
+  if (!d_base_bits) return fail(GCOW_ERR_INVALID, "null base bit offset");
+  return encode_impl(field, p, d_out, out_capacity, d_total_bits, d_workspace, workspace_bytes, d_index, index_stride,
+                     hip_stream, d_base_bits);
 }
 
 gcow_status gcow_decode_device(const zfp_input* field, const gcow_params* p, const void* d_in, size_t in_bytes,

@@ -721,9 +721,11 @@ __global__ __launch_bounds__(T) void k_count(FieldDesc F, Params p, uint32_t ran
 
 // Exclusive scan of the range totals (one workgroup). base[] gets nranges + 1 entries (last = total bits); the
 // 32-bit words two ranges share are zeroed so both sides can atomicOr into them; the stream's flush word too.
+// d_base (optional): the stream already holds *d_base bits (chunked / appended encode); every offset starts there and
+// the first range ORs its first word into the bits before it.
 __global__ __launch_bounds__(1024) void k_scan_ranges(const uint64_t* __restrict__ sums, uint32_t nranges,
                                                       uint64_t* __restrict__ base, uint64_t* __restrict__ total,
-                                                      uint32_t* __restrict__ out32)
+                                                      uint32_t* __restrict__ out32, const uint64_t* __restrict__ d_base)
 {
   __shared__ uint64_t part[1024];
   const uint32_t t = threadIdx.x;
@@ -739,14 +741,15 @@ __global__ __launch_bounds__(1024) void k_scan_ranges(const uint64_t* __restrict
     part[t] += y;
     __syncthreads();
   }
-  uint64_t run = part[t] - s;
+  const uint64_t b0 = d_base ? *d_base : 0ull;
+  uint64_t run = b0 + part[t] - s;
   for (uint32_t i = i0; i < i1; i++) {
     base[i] = run;
     if (i > 0 && (run & 31)) out32[run >> 5] = 0u;
     run += sums[i];
   }
   if (t == 1023) {
-    const uint64_t tot = part[1023];
+    const uint64_t tot = b0 + part[1023];
     base[nranges] = tot;
     if (total) *total = tot;
   }
@@ -1014,209 +1017,6 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
     base += tile_total;
     __syncthreads();
   }
-}
-
-// ------------------------------------------------------------------------------------------------ 1-D variable rate,
-// single pass (decoupled look-back)
-// One workgroup per tile of 256 U consecutive blocks, tiles handed out in launch order by an atomic counter (so every
-// predecessor of a tile is resident or done). Each lane codes U consecutive blocks with the closed-form coder; the
-// tile's codes are assembled in LDS at tile-relative bit offsets; the tile total is published at once and one wave
-// looks back over the predecessors' published totals for the tile's global bit offset; the LDS words are then stored
-// shifted by that offset mod 32. The two words a tile shares with its neighbours go to a side array that
-// k_var_fixup merges. The input is read once (the two-pass form reads it twice and walks its tiles in series).
-// Descriptor: bits 62-63 status (0 empty, 1 tile total, 2 inclusive prefix), bits 0-61 value, written and read as one
-// 8-byte agent-scope atomic, so the value travels with its flag (cdna_hip_programming.md Guideline 16, form R2).
-constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1ull;
-
-// U consecutive 4-value blocks starting at block bl (zeros past the end; padded gather for a partial last block)
-template <int DT, int U>
-__device__ __forceinline__ void load_blocks1d(const FieldDesc& F, uint64_t bl, float (&f)[U][4])
-{
-  const uint64_t nb = F.nblocks;
-  if (bl + U <= nb && 4 * (bl + U) <= F.n[0]) {
-#pragma unroll
-    for (int k = 0; k < U; k++) load_row4<DT>(F.data, (int64_t)(4 * (bl + k)), f[k]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < U; k++) {
-      f[k][0] = f[k][1] = f[k][2] = f[k][3] = 0.0f;
-      if (bl + k < nb) load_block1d<DT>(F.data, F.n[0], (uint32_t)(bl + k), f[k]);
-    }
-  }
-}
-
-// Variable-rate 1-D tile totals (one workgroup per tile of 256 U blocks): the count pass of the scan form.
-template <int DT, int U>
-__global__ __launch_bounds__(256) void k_count1d_var_tiles(FieldDesc F, Params p, uint64_t* __restrict__ sums)
-{
-  __shared__ uint16_t tab[80];
-  __shared__ uint32_t red[4];
-  const uint32_t tid = threadIdx.x;
-  if (tid < 80) tab[tid] = plane_entry4(tid);
-  __syncthreads();
-  const uint64_t bl = (uint64_t)blockIdx.x * (256u * U) + (uint64_t)tid * U;
-  float f[U][4];
-  load_blocks1d<DT, U>(F, bl, f);
-  uint32_t lsum = 0;
-#pragma unroll
-  for (int k = 0; k < U; k++) {
-    bool sp;
-    uint32_t len = encode_block1d_var<false>(f[k], tab, p.minexp, p.maxprec, nullptr, sp);
-    const bool valid = bl + k < F.nblocks;
-    if (sp && valid) {
-      CountWriter cw;
-      len = encode_block<1>(cw, f[k], p);
-    }
-    lsum += valid ? len : 0u;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
-  if ((tid & 63) == 0) red[tid >> 6] = lsum;
-  __syncthreads();
-  if (tid == 0) sums[blockIdx.x] = (uint64_t)red[0] + red[1] + red[2] + red[3];
-}
-
-// LOOKBACK: tile numbers from the atomic counter and the tile offset from the decoupled look-back over desc;
-// otherwise tile = blockIdx.x and its offset is rbase[tile] (exclusive scan of k_count1d_var_tiles' totals).
-template <int DT, int U, bool LOOKBACK>
-__global__ __launch_bounds__(256) void k_encode1d_var_sp(FieldDesc F, Params p, uint64_t* desc, uint32_t* ctr,
-                                                         const uint64_t* __restrict__ rbase,
-                                                         uint32_t* __restrict__ fix, uint32_t ntiles,
-                                                         uint32_t* __restrict__ out32, uint64_t* __restrict__ d_total,
-                                                         uint64_t* __restrict__ index, uint32_t index_shift)
-{
-  constexpr uint32_t T = 256, TB = T * U;
-  constexpr uint32_t LW = (TB * 160 + 31) / 32 + 2;  // worst-case tile bits (a block is at most 140) + shift slack
-  __shared__ uint64_t lds64[(LW + 1) / 2];
-  __shared__ uint32_t scan_sh[T / 64];
-  __shared__ uint16_t tab[80];
-  __shared__ uint32_t s_tile;
-  __shared__ uint64_t s_prefix;
-  uint32_t* lds = (uint32_t*)lds64;
-  const uint32_t tid = threadIdx.x;
-  if (LOOKBACK && tid == 0) s_tile = atomicAdd(ctr, 1u);
-  if (tid < 80) tab[tid] = plane_entry4(tid);
-  for (uint32_t j = tid; j < (LW + 1) / 2; j += T) lds64[j] = 0ull;
-  __syncthreads();
-  const uint32_t tile = LOOKBACK ? s_tile : blockIdx.x;
-  const uint64_t nb = F.nblocks;
-  const uint64_t bl = (uint64_t)tile * TB + (uint64_t)tid * U;  // the lane's first block
-  float f[U][4];
-  load_blocks1d<DT, U>(F, bl, f);
-  uint64_t c[U][3];
-  uint32_t len[U];
-  bool sp[U];
-  uint32_t lsum = 0;
-#pragma unroll
-  for (int k = 0; k < U; k++) {
-    len[k] = encode_block1d_var<true>(f[k], tab, p.minexp, p.maxprec, c[k], sp[k]);
-    const bool valid = bl + k < nb;
-    sp[k] = sp[k] && valid;
-    if (sp[k]) {
-      CountWriter cw;
-      len[k] = encode_block<1>(cw, f[k], p);
-    }
-    len[k] = valid ? len[k] : 0u;
-    lsum += len[k];
-  }
-  uint32_t agg;
-  const uint32_t excl = block_exclusive_scan<T>(lsum, &agg, scan_sh);
-  if (LOOKBACK && tid == 0)
-    __hip_atomic_store(desc + tile, (tile ? LB_AGG : LB_INC) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // codes into LDS at tile-relative bit offsets (64-bit LDS atomics: neighbouring lanes share qwords)
-  uint32_t o = excl;
-#pragma unroll
-  for (int k = 0; k < U; k++) {
-    if (len[k]) {
-      if (sp[k]) {
-        LdsWriter w{lds, o, o + len[k]};
-        encode_block<1>(w, f[k], p);
-      } else {
-        const uint32_t qw = o >> 6, sh = o & 63u;
-        const uint32_t nq = (sh + len[k] + 63) >> 6;  // 1..4 qwords touched
-        atomicOr((unsigned long long*)&lds64[qw], (unsigned long long)(c[k][0] << sh));
-        if (nq > 1) atomicOr((unsigned long long*)&lds64[qw + 1],
-                             (unsigned long long)((sh ? c[k][0] >> (64 - sh) : 0ull) | (c[k][1] << sh)));
-        if (nq > 2) atomicOr((unsigned long long*)&lds64[qw + 2],
-                             (unsigned long long)((sh ? c[k][1] >> (64 - sh) : 0ull) | (c[k][2] << sh)));
-        if (nq > 3) atomicOr((unsigned long long*)&lds64[qw + 3], (unsigned long long)(c[k][2] >> (64 - sh)));
-      }
-    }
-    o += len[k];
-  }
-  // decoupled look-back: wave 0 reads 64 predecessor descriptors per step, nearest first; it stops at the nearest
-  // inclusive prefix, summing the tile totals in between, and waits while any descriptor before that one is empty
-  if (!LOOKBACK) {
-    if (tid == 0) s_prefix = rbase[tile];
-  } else if (tid < 64) {
-    uint64_t prefix = 0;
-    if (tile) {
-      int64_t t = (int64_t)tile - 1;
-      uint32_t spins = 0;
-      for (;;) {
-        const int64_t i = t - (int64_t)tid;
-        const uint64_t v = i >= 0 ? __hip_atomic_load(desc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : LB_INC;
-        const uint64_t inc = __ballot((v >> 62) == 2u);
-        const uint64_t emp = __ballot((v >> 62) == 0u);
-        const uint32_t fi = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
-        const uint64_t upto = fi >= 63 ? ~0ull : ((2ull << fi) - 1ull);
-        if (emp & upto) {
-          if (++spins > (1u << 26)) break;  // bounded spin (predecessors are resident, so never expected)
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        unsigned long long s = tid <= fi ? (v & LB_VAL) : 0ull;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-        prefix += s;
-        if (fi < 64) break;
-        t -= 64;
-      }
-    }
-    if (tid == 0) {
-      if (tile) __hip_atomic_store(desc + tile, LB_INC | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_prefix = prefix;
-    }
-  }
-  __syncthreads();
-  const uint64_t base = s_prefix;
-  const uint32_t lb = (uint32_t)(base & 31u);
-  const uint32_t W = (lb + agg + 31) >> 5;
-  const bool last = tile == ntiles - 1;
-  const bool tailp = ((lb + agg) & 31u) != 0;
-  const uint64_t gw0 = base >> 5;
-  for (uint32_t j = tid; j < W; j += T) {
-    const uint32_t v = lb ? ((lds[j] << lb) | (j ? lds[j - 1] >> (32 - lb) : 0u)) : lds[j];
-    if (j == 0 && lb) fix[2 * tile] = v;                           // shared with the previous tile
-    else if (j == W - 1 && tailp && !last) fix[2 * tile + 1] = v;  // shared with the next tile
-    else out32[gw0 + j] = v;
-  }
-  if (index) {
-    uint64_t oo = base + excl;
-#pragma unroll
-    for (int k = 0; k < U; k++) {
-      const uint64_t b = bl + k;
-      if (b < nb && (b & ((1ull << index_shift) - 1)) == 0) index[b >> index_shift] = oo;
-      oo += len[k];
-    }
-  }
-  if (last && tid == 0) {
-    const uint64_t E = base + agg;
-    if (d_total) *d_total = E;
-    const uint64_t ew = (E + 31) >> 5;
-    if (ew & 1) out32[ew] = 0u;  // stream_flush: zero-pad to a 64-bit boundary
-  }
-}
-
-// The word holding tile t's first bit (when not 32-bit aligned) = tile t-1's tail bits | tile t's head bits.
-// starts: look-back descriptors (flagged: inclusive prefix of tile t-1) or the scanned tile offsets (tile t's start).
-__global__ void k_var_fixup(const uint64_t* __restrict__ starts, int flagged, const uint32_t* __restrict__ fix,
-                            uint32_t ntiles, uint32_t* __restrict__ out32)
-{
-  const uint32_t t = blockIdx.x * 256u + threadIdx.x + 1u;
-  if (t >= ntiles) return;
-  const uint64_t s = flagged ? (starts[t - 1] & LB_VAL) : starts[t];  // first bit of tile t
-  if (s & 31u) out32[s >> 5] = fix[2 * (t - 1) + 1] | fix[2 * t];
 }
 
 // ------------------------------------------------------------------------------------------------ decode
@@ -1740,7 +1540,7 @@ hipError_t launch_encode_fixed1d(const void* in, int dtype, uint64_t nvals, uint
 template <int D, int DT, uint32_t T>
 static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const TilePlan& plan, uint32_t* out32,
                                  uint64_t* ws_sums, uint64_t* ws_base, uint64_t* d_total, uint64_t* index,
-                                 uint32_t index_shift, hipStream_t st)
+                                 uint32_t index_shift, const uint64_t* d_base, hipStream_t st)
 {
   const size_t lds = (size_t)plan.lds_words * 4;
   if (plan.fixed) {
@@ -1750,36 +1550,9 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
     return hipGetLastError();
   }
   const bool var1d = D == 1 && T == 256 && p.minbits <= 1 && p.maxbits >= 160 && !getenv("GCOW_GENERIC_VAR");
-  if constexpr (D == 1 && T == 256) {
-    const char* vm = getenv("GCOW_VAR1D_MODE");  // "2pass" (range form), "lookback" (single pass); default scan
-    const bool lookback = vm && !strcmp(vm, "lookback");
-    if (var1d && F.vec && !(vm && !strcmp(vm, "2pass"))) {  // tile forms; ws_sums is the workspace start
-      const uint32_t ntiles = var1d_sp_tiles(F.nblocks);
-      if (lookback) {
-        uint64_t* desc = ws_sums;
-        uint32_t* ctr = (uint32_t*)(desc + ((ntiles + 1) & ~1u));
-        uint32_t* fix = ctr + 4;
-        hipError_t e = hipMemsetAsync(desc, 0, (size_t)((ntiles + 1) & ~1u) * 8 + 16, st);
-        if (e != hipSuccess) return e;
-        k_encode1d_var_sp<DT, 2, true><<<ntiles, 256, 0, st>>>(F, p, desc, ctr, nullptr, fix, ntiles, out32, d_total,
-                                                               index, index_shift);
-        if (ntiles > 1) k_var_fixup<<<(ntiles - 1 + 255) / 256, 256, 0, st>>>(desc, 1, fix, ntiles, out32);
-      } else {
-        uint64_t* sums = ws_sums;
-        uint64_t* base = sums + ntiles;
-        uint32_t* fix = (uint32_t*)(base + ntiles + 1);
-        k_count1d_var_tiles<DT, 2><<<ntiles, 256, 0, st>>>(F, p, sums);
-        k_scan_ranges<<<1, 1024, 0, st>>>(sums, ntiles, base, d_total, out32);
-        k_encode1d_var_sp<DT, 2, false><<<ntiles, 256, 0, st>>>(F, p, nullptr, nullptr, base, fix, ntiles, out32,
-                                                                d_total, index, index_shift);
-        if (ntiles > 1) k_var_fixup<<<(ntiles - 1 + 255) / 256, 256, 0, st>>>(base, 0, fix, ntiles, out32);
-      }
-      return hipGetLastError();
-    }
-  }
   if (var1d) k_count1d_var<DT><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   else k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
-  k_scan_ranges<<<1, 1024, 0, st>>>(ws_sums, plan.nranges, ws_base, d_total, out32);
+  k_scan_ranges<<<1, 1024, 0, st>>>(ws_sums, plan.nranges, ws_base, d_total, out32, d_base);
   if (var1d) {
     k_encode1d_var<DT><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_base, out32, index, index_shift);
     return hipGetLastError();
@@ -1792,13 +1565,13 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
 
 hipError_t launch_encode_tiles(const FieldDesc& F, const Params& p, const TilePlan& plan, uint32_t* out32,
                                uint64_t* ws_sums, uint64_t* ws_base, uint64_t* d_total, uint64_t* index,
-                               uint32_t index_shift, void* stream)
+                               uint32_t index_shift, const uint64_t* d_base, void* stream)
 {
   hipStream_t st = S(stream);
   const bool bf = F.dtype == DT_BF16;
 #define GCOW_TILES(D, T)                                                                                       \
-  return bf ? launch_tiles_t<D, DT_BF16, T>(F, p, plan, out32, ws_sums, ws_base, d_total, index, index_shift, st) \
-            : launch_tiles_t<D, DT_F32, T>(F, p, plan, out32, ws_sums, ws_base, d_total, index, index_shift, st)
+  return bf ? launch_tiles_t<D, DT_BF16, T>(F, p, plan, out32, ws_sums, ws_base, d_total, index, index_shift, d_base, st) \
+            : launch_tiles_t<D, DT_F32, T>(F, p, plan, out32, ws_sums, ws_base, d_total, index, index_shift, d_base, st)
   if (F.dims == 1) {
     if (plan.threads == 256) { GCOW_TILES(1, 256); } else { GCOW_TILES(1, 64); }
   } else if (F.dims == 2) {

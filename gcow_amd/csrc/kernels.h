@@ -29,16 +29,11 @@ struct TilePlan {
   bool fixed;          // minbits == maxbits: offsets are b * maxbits
 };
 
-// Tile forms of the variable-rate 1-D encoder (k_count1d_var_tiles / k_encode1d_var_sp): tiles of 512 blocks;
-// workspace = tile totals + scanned offsets (+1) + two boundary words per tile (the look-back form needs less).
-inline uint32_t var1d_sp_tiles(uint64_t nblocks) { return (uint32_t)((nblocks + 511) / 512); }
-inline size_t var1d_sp_workspace(uint64_t nblocks) { return 24 * (size_t)var1d_sp_tiles(nblocks) + 32; }
-
 hipError_t launch_encode_fixed1d(const void* in, int dtype, uint64_t nvals, uint32_t nblocks, const Params& p,
                                  void* out, void* stream);
 hipError_t launch_encode_tiles(const FieldDesc& F, const Params& p, const TilePlan& plan, uint32_t* out32,
                                uint64_t* ws_sums, uint64_t* ws_base, uint64_t* d_total, uint64_t* index,
-                               uint32_t index_shift, void* stream);
+                               uint32_t index_shift, const uint64_t* d_base, void* stream);
 hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
                          uint32_t chunk, uint64_t nchunks, bool fixed, uint64_t base_bits, uint64_t* end_out,
                          void* stream);

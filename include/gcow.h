@@ -222,6 +222,21 @@ gcow_status gcow_encode_device(const zfp_input* field, const gcow_params* p, voi
                                uint64_t* d_index, uint32_t index_stride, void* hip_stream);
 
 /*
+ * Chunked encode of one variable-rate stream: append field's blocks to a stream whose first *d_base_bits bits (a
+ * DEVICE uint64) are already in d_out, as sw/'s stream_write_bits appends at the stream's current position
+ * (sw/src/stream.c:61-92), without the stream_flush padding a separate zfp_compress call would insert
+ * (sw/src/zfp.c:10-28). Encoding an array in chunks this way is byte-identical to one gcow_encode_device call on
+ * the whole array; *d_total_bits = *d_base_bits + the chunk's bits, so it is the next chunk's base. d_out must hold
+ * the previous bits plus gcow_max_output_bytes(field, p) (only the latter is checked against out_capacity). Block
+ * index entries (d_index) are absolute stream offsets. Fixed-rate streams are chunked by offsetting d_out on the
+ * host instead (GCOW_ERR_UNSUPPORTED here).
+ */
+gcow_status gcow_encode_device_append(const zfp_input* field, const gcow_params* p, void* d_out, size_t out_capacity,
+                                      const uint64_t* d_base_bits, uint64_t* d_total_bits, void* d_workspace,
+                                      size_t workspace_bytes, uint64_t* d_index, uint32_t index_stride,
+                                      void* hip_stream);
+
+/*
  * Decode d_in into field->data (DEVICE fp32 pointer) with libzfp 0.5.5 semantics. Fixed-rate streams
  * (minbits == maxbits) decode one block per thread; variable-rate streams need the index written by
  * gcow_encode_device (d_index/index_stride), or, with d_index == NULL, are decoded by a single sequential GPU lane.

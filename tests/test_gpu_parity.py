@@ -558,3 +558,53 @@ def test_var1d_single_pass_tiles(gc, orc, nblocks, mode):
         a[hit] = rng.standard_normal(hit.size).astype(np.float32)
         op = orc.accuracy(1e-6)
     _check_vs_oracle(gc, orc, a, op, index_stride=16)
+
+
+@pytest.mark.parametrize("mode", ["acc1e-6", "acc1e-3", "bf16_acc1e-6", "prec20"])
+def test_encode_append_chunks(gc, orc, mode):
+    """gcow_encode_device_append: a bucket encoded in uneven chunks, each appended at the device-side end of the
+    previous one, equals the oracle's single stream (and its block index is absolute)."""
+    a = np.concatenate([orc.gen_normal(4 * 3001 + 2, 1e-3, 41, True), _adversarial_1d(5)[:4 * 997]])
+    op = {"acc1e-6": orc.accuracy(1e-6), "acc1e-3": orc.accuracy(1e-3), "bf16_acc1e-6": orc.accuracy(1e-6),
+          "prec20": orc.precision(20)}[mode]
+    if mode.startswith("bf16"):
+        a = (a.view(np.uint32) >> 16).astype(np.uint16)
+    w_ref, bits_ref = orc.compress(a, op)
+    x = torch.from_numpy(a).cuda()
+    if a.dtype == np.uint16:
+        x = x.view(torch.bfloat16)
+    params = P(gc, op)
+    words = torch.zeros(gc.max_output_bytes(x.shape, params, x.dtype) // 8 + 4, dtype=torch.int64, device="cuda")
+    cuts = [0, 4 * 700, 4 * 701 + 0, 4 * 2500, 4 * 2516, a.size]  # an empty chunk, a 1-block chunk, a partial tail
+    bits = torch.zeros(len(cuts), dtype=torch.int64, device="cuda")
+    for i in range(len(cuts) - 1):
+        gc.encode_append(x[cuts[i]:cuts[i + 1]], params, words, bits[i:i + 1], bits[i + 1:i + 2])
+    torch.cuda.synchronize()
+    assert int(bits[-1]) == bits_ref
+    nw = (bits_ref + 63) // 64
+    assert np.array_equal(words[:nw].cpu().numpy().view(np.uint64), w_ref.view(np.uint64)[:nw])
+
+
+@pytest.mark.parametrize("mode", ["rate16", "rate8", "acc1e-6", "bf16_acc1e-3"])
+def test_host_encoder_pipelined(gc, orc, mode):
+    """HostEncoder (pinned host in -> overlapped H2D / encode / D2H in chunks -> pinned host out) equals the oracle."""
+    a = orc.gen_normal(4 * 40000 + 3, 1e-3, 43, True)
+    op = {"rate16": orc.rate(16, 1), "rate8": orc.rate(8, 1), "acc1e-6": orc.accuracy(1e-6),
+          "bf16_acc1e-3": orc.accuracy(1e-3)}[mode]
+    if mode.startswith("bf16"):
+        a = (a.view(np.uint32) >> 16).astype(np.uint16)
+    w_ref, bits_ref = orc.compress(a, op)
+    h = torch.from_numpy(a)
+    dtype = torch.float32
+    if a.dtype == np.uint16:
+        h, dtype = h.view(torch.bfloat16), torch.bfloat16
+    h = h.pin_memory()
+    params = P(gc, op)
+    enc = gc.HostEncoder(a.size, dtype, params, chunks=5)
+    out = torch.zeros(gc.max_output_bytes((a.size,), params, dtype) // 8 + 2, dtype=torch.int64).pin_memory()
+    for _ in range(2):  # reusable
+        out.zero_()
+        bits = enc(h, out)
+        assert bits == bits_ref
+        nw = (bits + 63) // 64
+        assert np.array_equal(out[:nw].numpy().view(np.uint64), w_ref.view(np.uint64)[:nw])
