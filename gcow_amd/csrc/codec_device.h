@@ -252,6 +252,53 @@ struct RegWriter64 {
   __device__ __forceinline__ void skip(uint32_t n) { pos += n; }
 };
 
+// One lane's private run of 32-bit words (LDS), written a whole word at a time: no atomics, no zeroing. For
+// fixed-rate blocks whose budget is a multiple of 32 bits, so each block owns its words. Bits past `limit` are
+// dropped (the budgeted coder's output is that prefix); finish() zero-fills the rest of the block's words.
+struct LaneWordWriter {
+  uint32_t* w;
+  uint64_t acc;
+  uint32_t fill, pos, limit;
+  __device__ __forceinline__ void put(uint64_t v, uint32_t n)
+  {
+    if (pos >= limit || n == 0) {
+      pos += n;
+      return;
+    }
+    if (n > limit - pos) {
+      n = limit - pos;
+      v &= lowmask64(n);
+    }
+    pos += n;
+    const uint64_t hi = fill ? (v >> (64 - fill)) : 0ull;  // bits of v past acc's 64
+    acc |= v << fill;
+    fill += n;  // <= 95
+    if (fill >= 32) {
+      *w++ = (uint32_t)acc;
+      acc = (acc >> 32) | (hi << 32);
+      fill -= 32;
+      if (fill >= 32) {
+        *w++ = (uint32_t)acc;
+        acc >>= 32;
+        fill -= 32;
+      }
+    }
+  }
+  __device__ __forceinline__ void skip(uint32_t n)
+  {
+    while (n) {
+      const uint32_t k = n < 64 ? n : 64;
+      put(0ull, k);
+      n -= k;
+    }
+  }
+  __device__ __forceinline__ void finish(uint32_t* end)
+  {
+    if (fill) *w++ = (uint32_t)acc;
+    while (w < end) *w++ = 0u;
+  }
+};
+
 // Bits OR-ed into a zero-initialised LDS window of 32-bit words at a local bit offset.
 struct LdsWriter {
   uint32_t* lds;
@@ -414,11 +461,36 @@ struct BitReader {
   }
 };
 
+// Reader over one block's 32-bit words staged in LDS (two zero pad words after the block).
+struct WordBitReader {
+  const uint32_t* w;
+  uint64_t pos;
+  __device__ __forceinline__ uint64_t peek64() const
+  {
+    const uint32_t i = (uint32_t)(pos >> 5), sh = (uint32_t)(pos & 31);
+    const uint64_t v = ((uint64_t)w[i] | ((uint64_t)w[i + 1] << 32)) >> sh;
+    return sh ? v | ((uint64_t)w[i + 2] << (64 - sh)) : v;
+  }
+  __device__ __forceinline__ uint64_t get(uint32_t n)
+  {
+    if (!n) return 0;
+    uint64_t v = peek64() & lowmask64(n);
+    pos += n;
+    return v;
+  }
+  __device__ __forceinline__ uint32_t bit()
+  {
+    uint32_t b = (w[pos >> 5] >> (pos & 31)) & 1u;
+    pos++;
+    return b;
+  }
+};
+
 // decode_ints (libzfp 0.5.5; sw/src/decode.c:141-183 with block size 4^d). The unary scan of each group test
 // (`for (; n < size - 1 && bits && (bits--, !read_bit()); n++)`) is done with one count-trailing-zeros of the next
 // 64 stream bits instead of bit by bit.
-template <int B>
-__device__ __forceinline__ uint32_t decode_ints(BitReader& r, uint32_t maxbits, uint32_t maxprec, uint32_t* u)
+template <int B, class Rd>
+__device__ __forceinline__ uint32_t decode_ints(Rd& r, uint32_t maxbits, uint32_t maxprec, uint32_t* u)
 {
   const int kmin = maxprec < 32 ? 32 - (int)maxprec : 0;
   uint32_t bits = maxbits;
@@ -463,8 +535,8 @@ __device__ __forceinline__ float dequant_scale(int emax)
 }
 
 // decode_fblock (decode.c:220-253 with libzfp semantics). Writes B floats to f.
-template <int D>
-__device__ __forceinline__ void decode_block(BitReader& r, const Params& p, float* f)
+template <int D, class Rd>
+__device__ __forceinline__ void decode_block(Rd& r, const Params& p, float* f)
 {
   constexpr int B = Dim<D>::B;
   uint32_t bits = 1;

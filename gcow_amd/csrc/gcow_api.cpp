@@ -171,6 +171,11 @@ gcow_status encode_impl(const zfp_input* field, const gcow_params* p, void* d_ou
     if (d_total_bits) GCOW_HIP(gcow::launch_set_u64(d_total_bits, (uint64_t)F.nblocks * p->maxbits, stream));
     return GCOW_OK;
   }
+  if (F.dims == 3 && p->minbits == p->maxbits && !d_index && gcow::fixed3d_ok(p->maxbits)) {
+    GCOW_HIP(gcow::launch_encode3d_fixed(F, pp, (uint32_t*)d_out, stream));
+    if (d_total_bits) GCOW_HIP(gcow::launch_set_u64(d_total_bits, (uint64_t)F.nblocks * p->maxbits, stream));
+    return GCOW_OK;
+  }
   const gcow::TilePlan pl = make_plan(F, *p);
   uint64_t *sums = nullptr, *base = nullptr;
   if (!pl.fixed) {
@@ -199,6 +204,10 @@ gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void
   if (fixed && F.dims == 1 && F.vec && (p->maxbits == 64 || p->maxbits == 32) && p->maxprec >= 32 &&
       p->minexp <= -154 && base_bits % 32 == 0 && !d_end && !getenv("GCOW_GENERIC_DECODE")) {
     GCOW_HIP(gcow::launch_decode_fixed1d(F, P(*p), (const uint64_t*)d_in, base_bits, stream));
+    return GCOW_OK;
+  }
+  if (fixed && F.dims == 3 && base_bits % 32 == 0 && !d_end && gcow::fixed3d_ok(p->maxbits)) {
+    GCOW_HIP(gcow::launch_decode3d_fixed(F, P(*p), (const uint32_t*)((const char*)d_in + base_bits / 8), stream));
     return GCOW_OK;
   }
   uint32_t chunk;

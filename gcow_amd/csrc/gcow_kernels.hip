@@ -1019,6 +1019,55 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
   }
 }
 
+// ------------------------------------------------------------------------------------------------ 3-D fixed rate
+// Fixed-rate 3-D blocks whose budget is a whole number of 32-bit words (maxbits = 32 WPB; rates 1, 2, 4, 8, 16, 32):
+// one block per lane, 256 consecutive blocks per workgroup. The lane codes its block (generic 64-coefficient coder,
+// encode.c:457-495 with libzfp's 3-D transform and perm_3) into its own LDS words through LaneWordWriter -- whole
+// words, no atomics -- and the workgroup then stores its 256 WPB contiguous stream words coalesced.
+template <int DT, uint32_t WPB>
+__global__ __launch_bounds__(256) void k_encode3d_fixed(FieldDesc F, Params p, uint32_t* __restrict__ out32)
+{
+  extern __shared__ uint32_t lds_w[];  // 256 x (WPB + 1) words (odd stride: conflict-free per-lane words)
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * 256u;
+  const uint32_t nvalid = min(256u, F.nblocks - b0);
+  uint32_t* mine = lds_w + tid * (WPB + 1);
+  if (tid < nvalid) {
+    float f[64];
+    gather_block<3, DT>(F, b0 + tid, f);
+    LaneWordWriter w{mine, 0ull, 0u, 0u, WPB * 32u};
+    encode_block<3>(w, f, p);
+    w.finish(mine + WPB);
+  }
+  __syncthreads();
+  uint32_t* dst = out32 + (uint64_t)b0 * WPB;
+  for (uint32_t j = tid; j < nvalid * WPB; j += 256) dst[j] = lds_w[(j / WPB) * (WPB + 1) + (j % WPB)];
+  if (blockIdx.x == gridDim.x - 1 && tid == 0 && (((uint64_t)F.nblocks * WPB) & 1))
+    out32[(uint64_t)F.nblocks * WPB] = 0u;  // stream_flush: zero-pad to a 64-bit boundary
+}
+
+// The matching decoder: the workgroup stages its 256 blocks' stream words in LDS (coalesced), each lane decodes its
+// block from LDS (libzfp decode semantics) and scatters it.
+template <uint32_t WPB>
+__global__ __launch_bounds__(256) void k_decode3d_fixed(FieldDesc F, Params p, const uint32_t* __restrict__ in32)
+{
+  extern __shared__ uint32_t lds_w[];  // 256 x (WPB + 2) words: the block, then two zero pad words for peek64
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * 256u;
+  const uint32_t nvalid = min(256u, F.nblocks - b0);
+  const uint32_t* src = in32 + (uint64_t)b0 * WPB;
+  for (uint32_t j = tid; j < nvalid * WPB; j += 256) lds_w[(j / WPB) * (WPB + 2) + (j % WPB)] = src[j];
+  lds_w[tid * (WPB + 2) + WPB] = 0u;
+  lds_w[tid * (WPB + 2) + WPB + 1] = 0u;
+  __syncthreads();
+  if (tid < nvalid) {
+    WordBitReader r{lds_w + tid * (WPB + 2), 0};
+    float f[64];
+    decode_block<3>(r, p, f);
+    scatter_block<3>(F, b0 + tid, f);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ decode
 template <int D>
 __global__ __launch_bounds__(64) void k_decode(FieldDesc F, Params p, const uint64_t* __restrict__ in,
@@ -1593,6 +1642,64 @@ hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in
   else if (F.dims == 2) k_decode<2><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
   else k_decode<3><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
   return hipGetLastError();
+}
+
+template <int DT, uint32_t WPB>
+static hipError_t launch_enc3d_t(const FieldDesc& F, const Params& p, uint32_t* out32, hipStream_t st)
+{
+  const size_t lds = 256 * (WPB + 1) * 4;
+  auto kern = k_encode3d_fixed<DT, WPB>;
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  kern<<<(F.nblocks + 255) / 256, 256, lds, st>>>(F, p, out32);
+  return hipGetLastError();
+}
+
+template <uint32_t WPB>
+static hipError_t launch_dec3d_t(const FieldDesc& F, const Params& p, const uint32_t* in32, hipStream_t st)
+{
+  const size_t lds = 256 * (WPB + 2) * 4;
+  auto kern = k_decode3d_fixed<WPB>;
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  kern<<<(F.nblocks + 255) / 256, 256, lds, st>>>(F, p, in32);
+  return hipGetLastError();
+}
+
+bool fixed3d_ok(uint32_t maxbits)
+{
+  const uint32_t w = maxbits / 32;
+  return maxbits % 32 == 0 && (w == 2 || w == 4 || w == 8 || w == 16 || w == 32 || w == 64) &&
+         !getenv("GCOW_GENERIC_3D");
+}
+
+hipError_t launch_encode3d_fixed(const FieldDesc& F, const Params& p, uint32_t* out32, void* stream)
+{
+  hipStream_t st = S(stream);
+  const bool bf = F.dtype == DT_BF16;
+#define GCOW_E3(W) return bf ? launch_enc3d_t<DT_BF16, W>(F, p, out32, st) : launch_enc3d_t<DT_F32, W>(F, p, out32, st)
+  switch (p.maxbits / 32) {
+    case 2: GCOW_E3(2);
+    case 4: GCOW_E3(4);
+    case 8: GCOW_E3(8);
+    case 16: GCOW_E3(16);
+    case 32: GCOW_E3(32);
+    case 64: GCOW_E3(64);
+  }
+#undef GCOW_E3
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_decode3d_fixed(const FieldDesc& F, const Params& p, const uint32_t* in32, void* stream)
+{
+  hipStream_t st = S(stream);
+  switch (p.maxbits / 32) {
+    case 2: return launch_dec3d_t<2>(F, p, in32, st);
+    case 4: return launch_dec3d_t<4>(F, p, in32, st);
+    case 8: return launch_dec3d_t<8>(F, p, in32, st);
+    case 16: return launch_dec3d_t<16>(F, p, in32, st);
+    case 32: return launch_dec3d_t<32>(F, p, in32, st);
+    case 64: return launch_dec3d_t<64>(F, p, in32, st);
+  }
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t base_bits,

@@ -41,6 +41,10 @@ hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in
 // base_bits % 32 == 0
 hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t base_bits,
                                  void* stream);
+// fixed-rate 3-D blocks of a whole number of 32-bit words (fixed3d_ok); decode needs base_bits % 32 == 0
+bool fixed3d_ok(uint32_t maxbits);
+hipError_t launch_encode3d_fixed(const FieldDesc& F, const Params& p, uint32_t* out32, void* stream);
+hipError_t launch_decode3d_fixed(const FieldDesc& F, const Params& p, const uint32_t* in32, void* stream);
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
 hipError_t launch_prepend_header(uint64_t* dst, uint32_t off, const uint64_t* src, const uint64_t* d_bits,
                                  const uint64_t* header, uint64_t max_words, uint64_t* d_total, void* stream);

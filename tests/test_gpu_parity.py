@@ -608,3 +608,19 @@ def test_host_encoder_pipelined(gc, orc, mode):
         assert bits == bits_ref
         nw = (bits + 63) // 64
         assert np.array_equal(out[:nw].numpy().view(np.uint64), w_ref.view(np.uint64)[:nw])
+
+
+@pytest.mark.parametrize("r", [1, 2, 4, 8, 16, 32, 2.5])
+def test_fixed3d_word_rates(gc, orc, r):
+    """Fixed-rate 3-D blocks through the per-lane word-writer encoder and the LDS-staged decoder (block budgets of
+    2..64 words; rate 2.5 = 160 bits takes the generic path), partial blocks on every axis, zero / tiny / Inf / NaN
+    blocks, fp32 and bf16, stream and decode vs the oracle."""
+    rng = np.random.default_rng(int(r * 10))
+    a = (rng.standard_normal((13, 17, 21)) * 1e-2).astype(np.float32)
+    a[:4, :4, :4] = 0
+    a[4:8, :4, :4] = 1e-36
+    a[8, 5, 5] = np.inf
+    a[12, 16, 20] = np.nan
+    _check_vs_oracle(gc, orc, a, orc.rate(r, 3))
+    bf = (a.view(np.uint32) >> 16).astype(np.uint16)
+    _check_vs_oracle(gc, orc, bf, orc.rate(r, 3), decode=False)
