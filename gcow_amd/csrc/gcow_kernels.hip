@@ -823,15 +823,15 @@ __global__ __launch_bounds__(T) void k_encode_tiles(FieldDesc F, Params p, uint3
 
 // ------------------------------------------------------------------------------------------------ 1-D variable rate
 // Closed-form coder for variable-rate 1-D blocks (accuracy / precision / expert modes whose budget never truncates a
-// block: minbits <= 1, maxbits >= 160). Same structure as lean-4, with the plane range ending at kmin = 32 - prec:
-//   header (9) | empty planes 31 .. max(M0, kmin - 1) + 1 ('0' each) | group phase M0 .. max(T2, kmin), one plane
-//   per wave-uniform step through the 80-entry plane table (lanes past their own group phase emit verbatim nibbles,
-//   lanes past kmin emit nothing) | verbatim nibbles down to kmin from the 32-plane window.
+// block: minbits <= 1, maxbits >= 160). Same structure as lean-5, with the plane range ending at kmin = 32 - prec:
+//   header (9) | empty planes 31 .. max(M0, kmin - 1) + 1 ('0' each) | group phase M0 .. max(T2, kmin), two planes
+//   per wave-uniform step through the pair table (lanes past their own group phase emit verbatim nibbles, lanes
+//   past kmin emit nothing) | verbatim nibbles down to kmin from the 32-plane window.
 // Returns the block's bit length; with CODE the bits in c[0..2] (a block is at most 140 bits). special: Inf/NaN, or a
 // group phase longer than 16 planes or 64 bits -> generic coder.
 template <bool CODE>
-__device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uint16_t* tab, int minexp,
-                                                      uint32_t maxprec, uint64_t* c, bool& special)
+__device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uint16_t* tab, const uint32_t* tab2,
+                                                      int minexp, uint32_t maxprec, uint64_t* c, bool& special)
 {
   const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
   const uint32_t a2 = __float_as_uint(f[2]) & 0x7fffffffu, a3 = __float_as_uint(f[3]) & 0x7fffffffu;
@@ -862,16 +862,27 @@ __device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uin
   uint64_t g = 0;  // group-phase bits, relative to pos0
   uint32_t glen = 0, n = 0;
   int j = 0;
+  // two planes per step through the lean-5 pair table (tab2: n' << 10 | len << 13 | code << 17); a pair whose second
+  // plane is below kmin takes its first plane's code from the single-plane table (tab)
 #pragma unroll
-  for (; j < 16; j++) {
+  for (; j < 16; j += 2) {
     if (!__any(j <= jg)) break;
-    const uint32_t e = tab[(n << 4) | ((uint32_t)(Y >> (4 * j)) & 15u)];
-    const bool act = j < nplanes;
-    const uint32_t len = act ? (e >> 7) & 7u : 0u;
-    if (CODE) g |= (uint64_t)(act && glen < 64 ? (e & 127u) : 0u) << glen;
+    const uint32_t byte = (uint32_t)(Y >> (4 * j)) & 255u;
+    const uint32_t e = tab2[(n << 8) | byte];
+    const bool act2 = j + 1 < nplanes, act1 = j < nplanes;
+    uint32_t code = act2 ? e >> 17 : 0u, len = act2 ? (e >> 13) & 15u : 0u;
+    if (__any(act1 && !act2)) {
+      const uint32_t e1 = tab[(n << 4) | (byte & 15u)];
+      if (act1 && !act2) {
+        code = e1 & 127u;
+        len = (e1 >> 7) & 7u;
+      }
+    }
+    if (CODE) g |= (uint64_t)(glen < 64 ? code : 0u) << glen;
     glen += len;
-    n = act ? e >> 10 : n;
+    n = act2 ? (e >> 10) & 7u : n;
   }
+  j = min(j, 16);
   special = special || jg >= 16 || glen > 64;
   const int tplanes = max(nplanes - j, 0);  // verbatim planes after the group phase
   const uint32_t len = pos0 + glen + 4u * (uint32_t)tplanes;
@@ -910,6 +921,8 @@ template <int DT>
 __global__ __launch_bounds__(256) void k_count1d_var(FieldDesc F, Params p, uint32_t range, uint64_t* __restrict__ sums)
 {
   __shared__ uint16_t tab[80];
+  __shared__ uint32_t tab2[1280];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab5.v[t];
   __shared__ uint64_t red[4];
   if (threadIdx.x < 80) tab[threadIdx.x] = plane_entry4(threadIdx.x);
   __syncthreads();
@@ -921,7 +934,7 @@ __global__ __launch_bounds__(256) void k_count1d_var(FieldDesc F, Params p, uint
     float f[4] = {0, 0, 0, 0};
     if (b < b1) gather_block<1, DT>(F, (uint32_t)b, f);
     bool special;
-    uint32_t len = encode_block1d_var<false>(f, tab, p.minexp, p.maxprec, nullptr, special);
+    uint32_t len = encode_block1d_var<false>(f, tab, tab2, p.minexp, p.maxprec, nullptr, special);
     if (special && b < b1) {
       CountWriter w;
       len = encode_block<1>(w, f, p);
@@ -946,9 +959,11 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
   __shared__ uint64_t lds64[(31 + T * 160 + 63) / 64 + 4];
   __shared__ uint32_t scan_sh[T / 64];
   __shared__ uint16_t tab[80];
+  __shared__ uint32_t tab2[1280];
   uint32_t* lds = (uint32_t*)lds64;
   const uint32_t tid = threadIdx.x;
   if (tid < 80) tab[tid] = plane_entry4(tid);
+  for (uint32_t t = tid; t < 1280; t += T) tab2[t] = g_plane_tab5.v[t];
   const uint64_t b0 = (uint64_t)blockIdx.x * range;
   const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
   const bool final_range = b1 == F.nblocks;
@@ -964,7 +979,7 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
     if (valid) gather_block<1, DT>(F, (uint32_t)b, f);
     uint64_t c[3];
     bool special;
-    uint32_t len = encode_block1d_var<true>(f, tab, p.minexp, p.maxprec, c, special);
+    uint32_t len = encode_block1d_var<true>(f, tab, tab2, p.minexp, p.maxprec, c, special);
     special = special && valid;
     if (special) {
       CountWriter cw;
