@@ -8,6 +8,7 @@
               path (pinned H2D of the bf16 bucket + encode + D2H of the stream), sequential and overlapped in
               chunks (codec.HostEncoder)
   var_f32     256 Mi fp32 1-D accuracy 1e-6 / 1e-3 encode
+  var_decode  256 Mi fp32 1-D accuracy 1e-6 / 1e-3 decode (block index every 16 blocks)
 Timing: HIP events on the launching stream, median of interleaved rounds.
 """
 import argparse
@@ -100,6 +101,19 @@ def var_f32():
         e = enc(x)
         emit(case="var_f32_acc%g" % tol, ms=round(ms, 3), GiBps_input=round(n * 4 / (ms / 1e3) / 2 ** 30, 1),
              bits_per_value=round(e.bits / n, 3))
+
+
+def var_decode():
+    """1-D variable-rate decode (the receiving side of the compressed all-gather DDP hook): 256 Mi fp32, accuracy
+    1e-6 / 1e-3, block index every 16 blocks."""
+    n = 256 << 20
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    codec.fill_normal(x)
+    out = torch.empty_like(x)
+    for tol in (1e-6, 1e-3):
+        e = codec.encode(x, codec.accuracy(tol), index_stride=16)
+        ms = timeit(lambda: codec.decode(e, out=out), reps=3)
+        emit(case="var_decode_f32_acc%g" % tol, ms=round(ms, 3), GiBps_output=round(n * 4 / (ms / 1e3) / 2 ** 30, 1))
 
 
 def c5():
