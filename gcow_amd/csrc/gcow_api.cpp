@@ -225,6 +225,11 @@ gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void
     chunk = F.nblocks;  // no index: one sequential lane
     nchunks = 1;
   }
+  if (!fixed && F.dims == 1 && F.vec && p->minbits <= 1 && p->maxbits >= 160 && !getenv("GCOW_GENERIC_DECODE")) {
+    GCOW_HIP(gcow::launch_decode1d_var(F, P(*p), (const uint64_t*)d_in, d_index, chunk, nchunks, base_bits, d_end,
+                                       stream));
+    return GCOW_OK;
+  }
   GCOW_HIP(gcow::launch_decode(F, P(*p), (const uint64_t*)d_in, d_index, chunk, nchunks, fixed, base_bits, d_end,
                                stream));
   return GCOW_OK;

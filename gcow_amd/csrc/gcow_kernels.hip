@@ -1324,6 +1324,126 @@ __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restric
   }
 }
 
+// ------------------------------------------------------------------------------------------------ 1-D variable-rate
+// decode. Variable-rate 1-D streams whose budget never truncates a block (minbits <= 1, maxbits >= 160: accuracy,
+// precision, expert) decode block by block with the fixed-rate decoder's plane table instead of bit by bit: header,
+// then the empty planes (one '0' each: a count-trailing-zeros), the group phase (one (n, 7 stream bits) lookup per
+// plane while n < 3, down to kmin), then the remaining planes as a verbatim nibble run (a plane with n >= 3 is its
+// nibble) and the inverse bit transpose; libzfp decode_ints semantics (decode.c:141-183 with the block-size fix).
+// One lane per block-index chunk, blocks in sequence (each block's start is the previous block's end).
+__device__ __forceinline__ uint64_t stream_window(const uint64_t* in, uint64_t pos)
+{
+  const uint64_t i = pos >> 6;
+  const uint32_t sh = (uint32_t)(pos & 63);
+  const uint64_t lo = in[i] >> sh;
+  return sh ? lo | (in[i + 1] << (64 - sh)) : lo;
+}
+
+__device__ __forceinline__ void decode_block1d_var(const uint64_t* in, uint64_t& pos, const uint16_t* dtab, int minexp,
+                                                   uint32_t maxprec, float* f)
+{
+  uint64_t w = stream_window(in, pos);
+  if (!(w & 1u)) {  // zero block (or prec = 0): one 0 bit
+    f[0] = f[1] = f[2] = f[3] = 0.0f;
+    pos += 1;
+    return;
+  }
+  const int emax = (int)((w >> 1) & 255u) - 127;
+  const int prec = min((int)maxprec, max(0, emax - minexp + 4));
+  const int kmin = prec < 32 ? 32 - prec : 0;
+  const int np = 32 - kmin;  // coded planes 31 .. kmin
+  pos += 9;
+  w = stream_window(in, pos);
+  const int z = w ? (int)__builtin_ctzll(w) : 64;
+  uint32_t u[4] = {0u, 0u, 0u, 0u};
+  if (z >= np) {
+    pos += (uint32_t)np;  // every coded plane empty
+  } else {
+    pos += (uint32_t)z;
+    const int M0 = 31 - z;
+    const int nbelow = M0 - kmin + 1;  // planes M0 .. kmin
+    uint64_t Ylo = 0, Yhi = 0;         // plane nibbles M0 - j, j = 0..31
+    uint32_t n = 0, used = 0;
+    int j = 0;
+    w = stream_window(in, pos);
+    while (n < 3 && j < nbelow) {
+      if (used > 56) {
+        pos += used;
+        used = 0;
+        w = stream_window(in, pos);
+      }
+      const uint32_t e = dtab[(((n << 3) | 7u) << 7) | ((uint32_t)(w >> used) & 127u)];
+      const uint64_t nib = e & 15u;
+      if (j < 16) Ylo |= nib << (4 * j);
+      else Yhi |= nib << (4 * (j - 16));
+      used += (e >> 4) & 15u;
+      n = e >> 8;
+      j++;
+    }
+    pos += used;
+    const int t = nbelow - j;  // planes left: 4 bits each, verbatim
+    if (t > 0) {
+      const uint32_t nb = 4u * (uint32_t)t;  // <= 128
+      uint64_t v0 = stream_window(in, pos), v1 = nb > 64 ? stream_window(in, pos + 64) : 0ull;
+      if (nb < 64) v0 &= (1ull << nb) - 1ull;
+      else if (nb < 128) v1 &= (1ull << (nb - 64)) - 1ull;
+      const uint32_t sft = 4u * (uint32_t)j;  // nibble position of the run; sft + nb <= 128
+      if (sft == 0) {
+        Ylo |= v0;
+        Yhi |= v1;
+      } else if (sft < 64) {
+        Ylo |= v0 << sft;
+        Yhi |= (v0 >> (64 - sft)) | (v1 << sft);
+      } else {
+        Yhi |= v0 << (sft - 64);
+      }
+      pos += nb;
+    }
+    window_to_coeffs(Ylo, M0, u);
+    if (M0 >= 16) window_to_coeffs(Yhi, M0 - 16, u);
+  }
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = (int32_t)((u[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+  inv_lift(q[0], q[1], q[2], q[3]);
+  const float sc = dequant_scale(emax);
+#pragma unroll
+  for (int i = 0; i < 4; i++) f[i] = sc * (float)q[i];
+}
+
+__global__ __launch_bounds__(256) void k_decode1d_var(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                      const uint64_t* __restrict__ index, uint32_t chunk,
+                                                      uint64_t nchunks, uint64_t base_bits,
+                                                      uint64_t* __restrict__ end_out)
+{
+  __shared__ uint16_t dtab[5 * 8 * 128];
+  for (uint32_t t = threadIdx.x; t < 5 * 8 * 128 / 2; t += 256) ((uint32_t*)dtab)[t] = ((const uint32_t*)g_dec_tab1.v)[t];
+  __syncthreads();
+  const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (c >= nchunks) return;
+  uint64_t pos = base_bits + (index ? index[c] : 0ull);
+  const uint64_t b0 = c * chunk, b1 = min<uint64_t>(b0 + chunk, F.nblocks);
+  float* out = (float*)F.data;
+  if (chunk == 16 && 4 * b1 <= F.n[0] && b1 - b0 == 16) {
+    // the chunk's 256 output bytes are decoded into registers and stored in one burst: stored as they are decoded,
+    // every 128-B line stays half-written in L2 for most of the chunk's decode time
+    float g[16][4];
+#pragma unroll
+    for (int k = 0; k < 16; k++) decode_block1d_var(in, pos, dtab, p.minexp, p.maxprec, g[k]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) *(float4*)(out + 4 * (b0 + k)) = make_float4(g[k][0], g[k][1], g[k][2], g[k][3]);
+    if (end_out && c == nchunks - 1) *end_out = pos;
+    return;
+  }
+  for (uint64_t b = b0; b < b1; b++) {
+    float f[4];
+    decode_block1d_var(in, pos, dtab, p.minexp, p.maxprec, f);
+    if (4 * b + 4 <= F.n[0]) *(float4*)(out + 4 * b) = make_float4(f[0], f[1], f[2], f[3]);
+    else scatter_block<1>(F, (uint32_t)b, f);
+  }
+  if (end_out && c == nchunks - 1) *end_out = pos;
+}
+
 // the partial last block of a 1-D field (generic decoder, one lane)
 __global__ void k_decode_tail1d(FieldDesc F, Params p, const uint64_t* __restrict__ in, uint64_t base_bits,
                                 uint32_t b)
@@ -1715,6 +1835,14 @@ hipError_t launch_decode3d_fixed(const FieldDesc& F, const Params& p, const uint
     case 64: return launch_dec3d_t<64>(F, p, in32, st);
   }
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
+                               uint32_t chunk, uint64_t nchunks, uint64_t base_bits, uint64_t* end_out, void* stream)
+{
+  k_decode1d_var<<<(uint32_t)((nchunks + 255) / 256), 256, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, base_bits,
+                                                                           end_out);
+  return hipGetLastError();
 }
 
 hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t base_bits,
