@@ -192,7 +192,8 @@ gcow_status encode_impl(const zfp_input* field, const gcow_params* p, void* d_ou
 }
 
 gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void* d_in, const uint64_t* d_index,
-                        uint32_t index_stride, uint64_t base_bits, uint64_t* d_end, void* stream)
+                        uint32_t index_stride, uint64_t base_bits, uint64_t* d_end, void* stream,
+                        size_t in_bytes = 0)
 {
   gcow::FieldDesc F;
   gcow_status st = make_field(field, F, true);
@@ -226,8 +227,8 @@ gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void
     nchunks = 1;
   }
   if (!fixed && F.dims == 1 && F.vec && p->minbits <= 1 && p->maxbits >= 160 && !getenv("GCOW_GENERIC_DECODE")) {
-    GCOW_HIP(gcow::launch_decode1d_var(F, P(*p), (const uint64_t*)d_in, d_index, chunk, nchunks, base_bits, d_end,
-                                       stream));
+    GCOW_HIP(gcow::launch_decode1d_var(F, P(*p), (const uint64_t*)d_in, in_bytes / 8, d_index, chunk, nchunks,
+                                       base_bits, d_end, stream));
     return GCOW_OK;
   }
   GCOW_HIP(gcow::launch_decode(F, P(*p), (const uint64_t*)d_in, d_index, chunk, nchunks, fixed, base_bits, d_end,
@@ -731,8 +732,7 @@ gcow_status gcow_encode_device_append(const zfp_input* field, const gcow_params*
 gcow_status gcow_decode_device(const zfp_input* field, const gcow_params* p, const void* d_in, size_t in_bytes,
                                const uint64_t* d_index, uint32_t index_stride, void* hip_stream)
 {
-  (void)in_bytes;
-  return decode_impl(field, p, d_in, d_index, index_stride, 0, nullptr, hip_stream);
+  return decode_impl(field, p, d_in, d_index, index_stride, 0, nullptr, hip_stream, in_bytes);
 }
 
 // ---------------------------------------------------------------------------------------------- zfp header
@@ -885,8 +885,7 @@ gcow_status gcow_decode_device_at(const zfp_input* field, const gcow_params* p, 
                                   uint64_t bit_offset, const uint64_t* d_index, uint32_t index_stride,
                                   void* hip_stream)
 {
-  (void)in_bytes;
-  return decode_impl(field, p, d_in, d_index, index_stride, bit_offset, nullptr, hip_stream);
+  return decode_impl(field, p, d_in, d_index, index_stride, bit_offset, nullptr, hip_stream, in_bytes);
 }
 
 gcow_status gcow_stitch_device(uint64_t* d_dst, uint64_t dst_bit_offset, const uint64_t* d_src, uint64_t src_bits,

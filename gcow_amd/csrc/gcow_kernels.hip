@@ -1339,10 +1339,27 @@ __device__ __forceinline__ uint64_t stream_window(const uint64_t* in, uint64_t p
   return sh ? lo | (in[i + 1] << (64 - sh)) : lo;
 }
 
-__device__ __forceinline__ void decode_block1d_var(const uint64_t* in, uint64_t& pos, const uint16_t* dtab, int minexp,
+// 64 stream bits at a bit position, from global memory or from words staged in LDS (positions relative to them)
+struct GlobalWindow {
+  const uint64_t* in;
+  __device__ __forceinline__ uint64_t operator()(uint64_t pos) const { return stream_window(in, pos); }
+};
+struct LdsWindow {
+  const uint64_t* w;
+  __device__ __forceinline__ uint64_t operator()(uint64_t pos) const
+  {
+    const uint32_t i = (uint32_t)(pos >> 6), sh = (uint32_t)(pos & 63);
+    const uint64_t lo = w[i] >> sh;
+    return sh ? lo | (w[i + 1] << (64 - sh)) : lo;
+  }
+};
+
+// dtab: the full (n, r, 7 bits) plane table, or (COMPACT) its r = 7 rows only, indexed (n, 7 bits)
+template <class Win, bool COMPACT = true>
+__device__ __forceinline__ void decode_block1d_var(const Win& win, uint64_t& pos, const uint16_t* dtab, int minexp,
                                                    uint32_t maxprec, float* f)
 {
-  uint64_t w = stream_window(in, pos);
+  uint64_t w = win(pos);
   if (!(w & 1u)) {  // zero block (or prec = 0): one 0 bit
     f[0] = f[1] = f[2] = f[3] = 0.0f;
     pos += 1;
@@ -1353,7 +1370,7 @@ __device__ __forceinline__ void decode_block1d_var(const uint64_t* in, uint64_t&
   const int kmin = prec < 32 ? 32 - prec : 0;
   const int np = 32 - kmin;  // coded planes 31 .. kmin
   pos += 9;
-  w = stream_window(in, pos);
+  w = win(pos);
   const int z = w ? (int)__builtin_ctzll(w) : 64;
   uint32_t u[4] = {0u, 0u, 0u, 0u};
   if (z >= np) {
@@ -1365,14 +1382,14 @@ __device__ __forceinline__ void decode_block1d_var(const uint64_t* in, uint64_t&
     uint64_t Ylo = 0, Yhi = 0;         // plane nibbles M0 - j, j = 0..31
     uint32_t n = 0, used = 0;
     int j = 0;
-    w = stream_window(in, pos);
+    w = win(pos);
     while (n < 3 && j < nbelow) {
       if (used > 56) {
         pos += used;
         used = 0;
-        w = stream_window(in, pos);
+        w = win(pos);
       }
-      const uint32_t e = dtab[(((n << 3) | 7u) << 7) | ((uint32_t)(w >> used) & 127u)];
+      const uint32_t e = dtab[(COMPACT ? (n << 7) : ((((n << 3) | 7u)) << 7)) | ((uint32_t)(w >> used) & 127u)];
       const uint64_t nib = e & 15u;
       if (j < 16) Ylo |= nib << (4 * j);
       else Yhi |= nib << (4 * (j - 16));
@@ -1384,7 +1401,7 @@ __device__ __forceinline__ void decode_block1d_var(const uint64_t* in, uint64_t&
     const int t = nbelow - j;  // planes left: 4 bits each, verbatim
     if (t > 0) {
       const uint32_t nb = 4u * (uint32_t)t;  // <= 128
-      uint64_t v0 = stream_window(in, pos), v1 = nb > 64 ? stream_window(in, pos + 64) : 0ull;
+      uint64_t v0 = win(pos), v1 = nb > 64 ? win(pos + 64) : 0ull;
       if (nb < 64) v0 &= (1ull << nb) - 1ull;
       else if (nb < 128) v1 &= (1ull << (nb - 64)) - 1ull;
       const uint32_t sft = 4u * (uint32_t)j;  // nibble position of the run; sft + nb <= 128
@@ -1416,8 +1433,8 @@ __global__ __launch_bounds__(256) void k_decode1d_var(FieldDesc F, Params p, con
                                                       uint64_t nchunks, uint64_t base_bits,
                                                       uint64_t* __restrict__ end_out)
 {
-  __shared__ uint16_t dtab[5 * 8 * 128];
-  for (uint32_t t = threadIdx.x; t < 5 * 8 * 128 / 2; t += 256) ((uint32_t*)dtab)[t] = ((const uint32_t*)g_dec_tab1.v)[t];
+  __shared__ uint16_t dtab[5 * 128];  // r = 7 rows of the plane table
+  for (uint32_t t = threadIdx.x; t < 5 * 128; t += 256) dtab[t] = g_dec_tab1.v[(((t >> 7) << 3) | 7u) << 7 | (t & 127u)];
   __syncthreads();
   const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (c >= nchunks) return;
@@ -1429,7 +1446,7 @@ __global__ __launch_bounds__(256) void k_decode1d_var(FieldDesc F, Params p, con
     // every 128-B line stays half-written in L2 for most of the chunk's decode time
     float g[16][4];
 #pragma unroll
-    for (int k = 0; k < 16; k++) decode_block1d_var(in, pos, dtab, p.minexp, p.maxprec, g[k]);
+    for (int k = 0; k < 16; k++) decode_block1d_var(GlobalWindow{in}, pos, dtab, p.minexp, p.maxprec, g[k]);
 #pragma unroll
     for (int k = 0; k < 16; k++) *(float4*)(out + 4 * (b0 + k)) = make_float4(g[k][0], g[k][1], g[k][2], g[k][3]);
     if (end_out && c == nchunks - 1) *end_out = pos;
@@ -1437,10 +1454,61 @@ __global__ __launch_bounds__(256) void k_decode1d_var(FieldDesc F, Params p, con
   }
   for (uint64_t b = b0; b < b1; b++) {
     float f[4];
-    decode_block1d_var(in, pos, dtab, p.minexp, p.maxprec, f);
+    decode_block1d_var(GlobalWindow{in}, pos, dtab, p.minexp, p.maxprec, f);
     if (4 * b + 4 <= F.n[0]) *(float4*)(out + 4 * b) = make_float4(f[0], f[1], f[2], f[3]);
     else scatter_block<1>(F, (uint32_t)b, f);
   }
+  if (end_out && c == nchunks - 1) *end_out = pos;
+}
+
+// The same decoder with the workgroup's stream span staged in LDS first (128 lanes x 16-block chunks: the span runs
+// from chunk c0's index entry to chunk c0 + 128's, at most 128 x 16 x 160 bits): one coalesced copy instead of each
+// lane's chain of dependent global window loads.
+// Capacity: 80 bits per block on average; a workgroup whose span is larger decodes from global memory instead.
+// Only the no-budget rows (r = 7) of the plane table are needed here: 640 entries.
+template <uint32_t LANES>
+__global__ __launch_bounds__(LANES) void k_decode1d_var_staged(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                               uint64_t in_words, const uint64_t* __restrict__ index,
+                                                               uint64_t nchunks, uint64_t base_bits,
+                                                               uint64_t* __restrict__ end_out)
+{
+  constexpr uint32_t CAP = LANES * 16 * 80 / 64;
+  __shared__ uint16_t dt7[5 * 128];
+  __shared__ uint64_t sw[CAP + 2];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t t = tid; t < 5 * 128; t += LANES) dt7[t] = g_dec_tab1.v[(((t >> 7) << 3) | 7u) << 7 | (t & 127u)];
+  const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
+  const uint64_t w0 = (base_bits + index[c0]) >> 6;
+  const uint64_t wend = c0 + LANES < nchunks ? ((base_bits + index[c0 + LANES] + 63) >> 6) : in_words;
+  const uint64_t span = min<uint64_t>(wend, in_words) - w0;
+  const bool staged = span <= CAP;
+  if (staged)
+    for (uint32_t j = tid; j < (uint32_t)span + 2; j += LANES) sw[j] = w0 + j < in_words ? in[w0 + j] : 0ull;
+  __syncthreads();
+  const uint64_t c = c0 + tid;
+  if (c >= nchunks) return;
+  const uint64_t b0 = c * 16, b1 = min<uint64_t>(b0 + 16, F.nblocks);
+  float* out = (float*)F.data;
+  uint64_t pos = base_bits + index[c];
+  auto run = [&](const auto& win, uint64_t rel) {
+    pos -= rel;
+    if (4 * b1 <= F.n[0] && b1 - b0 == 16) {
+      float g[16][4];
+#pragma unroll
+      for (int k = 0; k < 16; k++) decode_block1d_var(win, pos, dt7, p.minexp, p.maxprec, g[k]);
+#pragma unroll
+      for (int k = 0; k < 16; k++) *(float4*)(out + 4 * (b0 + k)) = make_float4(g[k][0], g[k][1], g[k][2], g[k][3]);
+    } else {
+      for (uint64_t b = b0; b < b1; b++) {
+        float f[4];
+        decode_block1d_var(win, pos, dt7, p.minexp, p.maxprec, f);
+        scatter_block<1>(F, (uint32_t)b, f);
+      }
+    }
+    pos += rel;
+  };
+  if (staged) run(LdsWindow{sw}, 64 * w0);
+  else run(GlobalWindow{in}, 0);
   if (end_out && c == nchunks - 1) *end_out = pos;
 }
 
@@ -1837,9 +1905,20 @@ hipError_t launch_decode3d_fixed(const FieldDesc& F, const Params& p, const uint
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
-                               uint32_t chunk, uint64_t nchunks, uint64_t base_bits, uint64_t* end_out, void* stream)
+hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t in_words,
+                               const uint64_t* index, uint32_t chunk, uint64_t nchunks, uint64_t base_bits,
+                               uint64_t* end_out, void* stream)
 {
+  const char* vm = getenv("GCOW_VDEC");  // "global" / "staged256" (A/B); default staged, 128 lanes
+  if (index && chunk == 16 && in_words && !(vm && !strcmp(vm, "global"))) {
+    if (!(vm && !strcmp(vm, "staged256")))
+      k_decode1d_var_staged<128><<<(uint32_t)((nchunks + 127) / 128), 128, 0, S(stream)>>>(F, p, in, in_words, index,
+                                                                                            nchunks, base_bits, end_out);
+    else
+      k_decode1d_var_staged<256><<<(uint32_t)((nchunks + 255) / 256), 256, 0, S(stream)>>>(F, p, in, in_words, index,
+                                                                                            nchunks, base_bits, end_out);
+    return hipGetLastError();
+  }
   k_decode1d_var<<<(uint32_t)((nchunks + 255) / 256), 256, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, base_bits,
                                                                            end_out);
   return hipGetLastError();

@@ -46,8 +46,10 @@ bool fixed3d_ok(uint32_t maxbits);
 hipError_t launch_encode3d_fixed(const FieldDesc& F, const Params& p, uint32_t* out32, void* stream);
 hipError_t launch_decode3d_fixed(const FieldDesc& F, const Params& p, const uint32_t* in32, void* stream);
 // variable-rate 1-D, contiguous fp32 output, blocks never truncated (minbits <= 1, maxbits >= 160)
-hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
-                               uint32_t chunk, uint64_t nchunks, uint64_t base_bits, uint64_t* end_out, void* stream);
+// in_words: stream buffer size (0 = unknown: no LDS staging)
+hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t in_words,
+                               const uint64_t* index, uint32_t chunk, uint64_t nchunks, uint64_t base_bits,
+                               uint64_t* end_out, void* stream);
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
 hipError_t launch_prepend_header(uint64_t* dst, uint32_t off, const uint64_t* src, const uint64_t* d_bits,
                                  const uint64_t* header, uint64_t max_words, uint64_t* d_total, void* stream);
