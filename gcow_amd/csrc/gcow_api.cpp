@@ -232,7 +232,7 @@ gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void
     return GCOW_OK;
   }
   GCOW_HIP(gcow::launch_decode(F, P(*p), (const uint64_t*)d_in, d_index, chunk, nchunks, fixed, base_bits, d_end,
-                               stream));
+                               stream, in_bytes / 8));
   return GCOW_OK;
 }
 

@@ -1104,6 +1104,48 @@ __global__ __launch_bounds__(64) void k_decode(FieldDesc F, Params p, const uint
   if (end_out && c == nchunks - 1) *end_out = r.pos;
 }
 
+// One block per lane with the workgroup's stream span staged in LDS (coalesced copy) and read through
+// WordBitReader: blocks start at the block index (stride 1) or at b * maxbits (fixed rate). A span above the
+// capacity (1024 bits per block on average) decodes from global memory.
+template <int D>
+__global__ __launch_bounds__(64) void k_decode_staged(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                      uint64_t in_words, const uint64_t* __restrict__ index,
+                                                      uint32_t fixed, uint64_t base_bits,
+                                                      uint64_t* __restrict__ end_out)
+{
+  constexpr int B = Dim<D>::B;
+  constexpr uint32_t CAPW = 64 * 1024 / 32;  // 32-bit words
+  __shared__ uint32_t sw[CAPW + 4];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * 64, nb = F.nblocks;
+  auto start_of = [&](uint64_t b) { return base_bits + (fixed ? b * p.maxbits : index[b]); };
+  const uint64_t s0 = start_of(b0);
+  const uint64_t w0 = s0 >> 5;  // 32-bit word index
+  const uint64_t in_w32 = 2 * in_words;
+  const uint64_t wend = b0 + 64 < nb ? (start_of(b0 + 64) + 31) >> 5 : in_w32;
+  const uint64_t span = min<uint64_t>(wend, in_w32) - w0;
+  const bool staged = span <= CAPW;
+  const uint32_t* in32 = (const uint32_t*)in;
+  if (staged)
+    for (uint32_t j = tid; j < (uint32_t)span + 4; j += 64) sw[j] = w0 + j < in_w32 ? in32[w0 + j] : 0u;
+  __syncthreads();
+  const uint64_t b = b0 + tid;
+  if (b >= nb) return;
+  float f[B];
+  uint64_t end;
+  if (staged) {
+    WordBitReader r{sw, start_of(b) - 32 * w0};
+    decode_block<D>(r, p, f);
+    end = r.pos + 32 * w0;
+  } else {
+    BitReader r{in, start_of(b)};
+    decode_block<D>(r, p, f);
+    end = r.pos;
+  }
+  scatter_block<D>(F, (uint32_t)b, f);
+  if (end_out && b == nb - 1) *end_out = end;
+}
+
 // ------------------------------------------------------------------------------------------------ fast 1-D decode
 // Fixed-rate 1-D decoder for whole-word blocks (maxbits 64 / 32, kmin = 0), the inverse of the lean-4 encoder:
 //  * header: bit 0 = 0 -> zero block; else biased emax in bits 1..8;
@@ -1836,8 +1878,14 @@ hipError_t launch_encode_tiles(const FieldDesc& F, const Params& p, const TilePl
 
 hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
                          uint32_t chunk, uint64_t nchunks, bool fixed, uint64_t base_bits, uint64_t* end_out,
-                         void* stream)
+                         void* stream, uint64_t in_words)
 {
+  if (chunk == 1 && in_words && (fixed || index) && F.dims >= 2 && !getenv("GCOW_DECODE_GLOBAL")) {
+    const uint32_t g = (uint32_t)((F.nblocks + 63) / 64);
+    if (F.dims == 2) k_decode_staged<2><<<g, 64, 0, S(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
+    else k_decode_staged<3><<<g, 64, 0, S(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
+    return hipGetLastError();
+  }
   const uint32_t T = 64;
   const uint64_t grid = (nchunks + T - 1) / T;
   if (!grid) return hipSuccess;

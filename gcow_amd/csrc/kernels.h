@@ -34,9 +34,10 @@ hipError_t launch_encode_fixed1d(const void* in, int dtype, uint64_t nvals, uint
 hipError_t launch_encode_tiles(const FieldDesc& F, const Params& p, const TilePlan& plan, uint32_t* out32,
                                uint64_t* ws_sums, uint64_t* ws_base, uint64_t* d_total, uint64_t* index,
                                uint32_t index_shift, const uint64_t* d_base, void* stream);
+// in_words: stream buffer size in uint64 (0 = unknown: no LDS staging)
 hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
                          uint32_t chunk, uint64_t nchunks, bool fixed, uint64_t base_bits, uint64_t* end_out,
-                         void* stream);
+                         void* stream, uint64_t in_words = 0);
 // fixed-rate 1-D whole-word blocks (maxbits 64 / 32, maxprec >= 32, minexp <= -154), contiguous fp32 output,
 // base_bits % 32 == 0
 hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t base_bits,
