@@ -624,3 +624,14 @@ def test_fixed3d_word_rates(gc, orc, r):
     _check_vs_oracle(gc, orc, a, orc.rate(r, 3))
     bf = (a.view(np.uint32) >> 16).astype(np.uint16)
     _check_vs_oracle(gc, orc, bf, orc.rate(r, 3), decode=False)
+
+
+@pytest.mark.parametrize("shape", [(12, 12, 12), (40, 44), (4 * 4099 + 1,)])
+def test_staged_decode_wide_blocks(gc, orc, shape):
+    """LDS-staged decoders with spans over their capacity (precision 32 on values spread over 2^-60..2^10: blocks of
+    up to ~2100 bits in 3-D): the over-capacity workgroups decode from global memory; vs the oracle."""
+    rng = np.random.default_rng(len(shape))
+    a = (np.where(rng.random(shape) < 0.5, -1.0, 1.0) * 2.0 ** rng.uniform(-60, 10, shape)).astype(np.float32)
+    stride = 16 if len(shape) == 1 else 1
+    _check_vs_oracle(gc, orc, a, orc.precision(32), index_stride=stride)
+    _check_vs_oracle(gc, orc, a, orc.accuracy(1e-30), index_stride=stride)
