@@ -917,29 +917,38 @@ __device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uin
 }
 
 // Variable-rate 1-D pass 1: per-range sums of block bit lengths (closed-form coder; generic for special blocks).
-template <int DT>
+// Each lane codes U consecutive blocks per step (tile = 256 U blocks).
+template <int DT, int U>
 __global__ __launch_bounds__(256) void k_count1d_var(FieldDesc F, Params p, uint32_t range, uint64_t* __restrict__ sums)
 {
   __shared__ uint16_t tab[80];
   __shared__ uint32_t tab2[1280];
-  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab5.v[t];
   __shared__ uint64_t red[4];
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab5.v[t];
   if (threadIdx.x < 80) tab[threadIdx.x] = plane_entry4(threadIdx.x);
   __syncthreads();
   const uint64_t b0 = (uint64_t)blockIdx.x * range;
   const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
   uint64_t acc = 0;
-  for (uint64_t t0 = b0; t0 < b1; t0 += 256) {  // wave-uniform trip count (the coder uses wave votes)
-    const uint64_t b = t0 + threadIdx.x;
-    float f[4] = {0, 0, 0, 0};
-    if (b < b1) gather_block<1, DT>(F, (uint32_t)b, f);
-    bool special;
-    uint32_t len = encode_block1d_var<false>(f, tab, tab2, p.minexp, p.maxprec, nullptr, special);
-    if (special && b < b1) {
-      CountWriter w;
-      len = encode_block<1>(w, f, p);
+  for (uint64_t t0 = b0; t0 < b1; t0 += 256 * U) {  // wave-uniform trip count (the coder uses wave votes)
+    float f[U][4];
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const uint64_t b = t0 + (uint64_t)threadIdx.x * U + k;
+      f[k][0] = f[k][1] = f[k][2] = f[k][3] = 0.0f;
+      if (b < b1) gather_block<1, DT>(F, (uint32_t)b, f[k]);
     }
-    acc += b < b1 ? len : 0u;
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const uint64_t b = t0 + (uint64_t)threadIdx.x * U + k;
+      bool special;
+      uint32_t len = encode_block1d_var<false>(f[k], tab, tab2, p.minexp, p.maxprec, nullptr, special);
+      if (special && b < b1) {
+        CountWriter w;
+        len = encode_block<1>(w, f[k], p);
+      }
+      acc += b < b1 ? len : 0u;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
@@ -948,15 +957,16 @@ __global__ __launch_bounds__(256) void k_count1d_var(FieldDesc F, Params p, uint
   if (threadIdx.x == 0) sums[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-// Variable-rate 1-D pass 2: k_encode_tiles with the closed-form coder; each lane ORs its <= 140-bit code into the
-// tile's LDS window with 64-bit LDS atomics.
-template <int DT>
+// Variable-rate 1-D pass 2: k_encode_tiles with the closed-form coder over tiles of 256 U blocks (U consecutive
+// blocks per lane: U times the work per barrier round); each lane ORs its <= 140-bit codes into the tile's LDS window
+// with 64-bit LDS atomics.
+template <int DT, int U>
 __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uint32_t range,
                                                       const uint64_t* __restrict__ rbase, uint32_t* __restrict__ out32,
                                                       uint64_t* __restrict__ index, uint32_t index_shift)
 {
   constexpr uint32_t T = 256;
-  __shared__ uint64_t lds64[(31 + T * 160 + 63) / 64 + 4];
+  __shared__ uint64_t lds64[(31 + T * U * 160 + 63) / 64 + 4];
   __shared__ uint32_t scan_sh[T / 64];
   __shared__ uint16_t tab[80];
   __shared__ uint32_t tab2[1280];
@@ -972,22 +982,32 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
   const bool first_shared = (base & 31) != 0;
   uint32_t carry = 0;
   __syncthreads();
-  for (uint64_t t0 = b0; t0 < b1; t0 += T) {
-    const uint64_t b = t0 + tid;
-    const bool valid = b < b1;
-    float f[4] = {0, 0, 0, 0};
-    if (valid) gather_block<1, DT>(F, (uint32_t)b, f);
-    uint64_t c[3];
-    bool special;
-    uint32_t len = encode_block1d_var<true>(f, tab, tab2, p.minexp, p.maxprec, c, special);
-    special = special && valid;
-    if (special) {
-      CountWriter cw;
-      len = encode_block<1>(cw, f, p);
+  for (uint64_t t0 = b0; t0 < b1; t0 += T * U) {
+    float f[U][4];
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const uint64_t b = t0 + (uint64_t)tid * U + k;
+      f[k][0] = f[k][1] = f[k][2] = f[k][3] = 0.0f;
+      if (b < b1) gather_block<1, DT>(F, (uint32_t)b, f[k]);
     }
-    len = valid ? len : 0u;
+    uint64_t c[U][3];
+    uint32_t len[U];
+    bool sp[U];
+    uint32_t lsum = 0;
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const bool valid = t0 + (uint64_t)tid * U + k < b1;
+      len[k] = encode_block1d_var<true>(f[k], tab, tab2, p.minexp, p.maxprec, c[k], sp[k]);
+      sp[k] = sp[k] && valid;
+      if (sp[k]) {
+        CountWriter cw;
+        len[k] = encode_block<1>(cw, f[k], p);
+      }
+      len[k] = valid ? len[k] : 0u;
+      lsum += len[k];
+    }
     uint32_t tile_total;
-    const uint32_t excl = block_exclusive_scan<T>(len, &tile_total, scan_sh);
+    const uint32_t excl = block_exclusive_scan<T>(lsum, &tile_total, scan_sh);
     const uint32_t lbase = (uint32_t)(base & 31);
     const uint32_t end_local = lbase + tile_total;
     const uint32_t W = (end_local + 31) >> 5;
@@ -995,25 +1015,30 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
     __syncthreads();
     if (tid == 0) lds[0] |= carry;
     __syncthreads();
-    if (valid) {
-      const uint32_t o = lbase + excl;
-      if (special) {
-        LdsWriter w{lds, o, o + len};
-        encode_block<1>(w, f, p);
-      } else {
-        const uint32_t qw = o >> 6, sh = o & 63u;
-        const uint32_t nq = (sh + len + 63) >> 6;  // 1..4 qwords touched
-        atomicOr((unsigned long long*)&lds64[qw], (unsigned long long)(c[0] << sh));
-        if (nq > 1) atomicOr((unsigned long long*)&lds64[qw + 1],
-                             (unsigned long long)((sh ? c[0] >> (64 - sh) : 0ull) | (c[1] << sh)));
-        if (nq > 2) atomicOr((unsigned long long*)&lds64[qw + 2],
-                             (unsigned long long)((sh ? c[1] >> (64 - sh) : 0ull) | (c[2] << sh)));
-        if (nq > 3) atomicOr((unsigned long long*)&lds64[qw + 3], (unsigned long long)(c[2] >> (64 - sh)));
+    uint32_t o = lbase + excl;
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      if (len[k]) {
+        if (sp[k]) {
+          LdsWriter w{lds, o, o + len[k]};
+          encode_block<1>(w, f[k], p);
+        } else {
+          const uint32_t qw = o >> 6, sh = o & 63u;
+          const uint32_t nq = (sh + len[k] + 63) >> 6;  // 1..4 qwords touched
+          atomicOr((unsigned long long*)&lds64[qw], (unsigned long long)(c[k][0] << sh));
+          if (nq > 1) atomicOr((unsigned long long*)&lds64[qw + 1],
+                               (unsigned long long)((sh ? c[k][0] >> (64 - sh) : 0ull) | (c[k][1] << sh)));
+          if (nq > 2) atomicOr((unsigned long long*)&lds64[qw + 2],
+                               (unsigned long long)((sh ? c[k][1] >> (64 - sh) : 0ull) | (c[k][2] << sh)));
+          if (nq > 3) atomicOr((unsigned long long*)&lds64[qw + 3], (unsigned long long)(c[k][2] >> (64 - sh)));
+        }
+        const uint64_t b = t0 + (uint64_t)tid * U + k;
+        if (index && ((b & ((1ull << index_shift) - 1)) == 0)) index[b >> index_shift] = base + (o - lbase);
       }
-      if (index && ((b & ((1ull << index_shift) - 1)) == 0)) index[b >> index_shift] = base + excl;
+      o += len[k];
     }
     __syncthreads();
-    const bool last_tile = t0 + T >= b1;
+    const bool last_tile = t0 + T * U >= b1;
     const bool partial = (end_local & 31) != 0;
     const uint32_t Wstore = (last_tile || !partial) ? W : (end_local >> 5);
     const uint64_t gw0 = base >> 5;
@@ -1844,11 +1869,11 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
     return hipGetLastError();
   }
   const bool var1d = D == 1 && T == 256 && p.minbits <= 1 && p.maxbits >= 160 && !getenv("GCOW_GENERIC_VAR");
-  if (var1d) k_count1d_var<DT><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
+  if (var1d) k_count1d_var<DT, 4><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   else k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   k_scan_ranges<<<1, 1024, 0, st>>>(ws_sums, plan.nranges, ws_base, d_total, out32, d_base);
   if (var1d) {
-    k_encode1d_var<DT><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_base, out32, index, index_shift);
+    k_encode1d_var<DT, 4><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_base, out32, index, index_shift);
     return hipGetLastError();
   }
   auto kern = k_encode_tiles<D, DT, T, false>;
