@@ -149,7 +149,7 @@ def expert(minbits, maxbits, maxprec, minexp) -> Params:
 def _shape(shape):
     """shape given numpy-style (slowest first); oracle wants (nx, ny, nz) fastest first."""
     dims = len(shape)
-    n = (C.c_size_t * 3)(*(list(reversed(shape)) + [0] * (3 - dims)))
+    n = (C.c_size_t * 4)(*(list(reversed(shape)) + [0] * (4 - dims)))
     return dims, n
 
 

@@ -190,6 +190,12 @@ void orc_fwd_xform(int32_t* q, unsigned dims)
       for (y = 0; y < 4; y++)
         for (x = 0; x < 4; x++) fwd_lift(q + x + 4 * y, 16);
       break;
+    case 4: /* libzfp 0.5.5 fwd_xform_4: x, y, z, then w */
+      for (unsigned l = 0; l < 64; l++) fwd_lift(q + 4 * l, 1);
+      for (unsigned l = 0; l < 64; l++) fwd_lift(q + (l & 3) + 16 * (l >> 2), 4);
+      for (unsigned l = 0; l < 64; l++) fwd_lift(q + (l & 15) + 64 * (l >> 4), 16);
+      for (unsigned l = 0; l < 64; l++) fwd_lift(q + l, 64);
+      break;
   }
 }
 
@@ -213,6 +219,12 @@ void orc_inv_xform(int32_t* q, unsigned dims)
       for (z = 0; z < 4; z++)
         for (y = 0; y < 4; y++) inv_lift(q + 4 * y + 16 * z, 1);
       break;
+    case 4: /* w, z, y, then x */
+      for (unsigned l = 0; l < 64; l++) inv_lift(q + l, 64);
+      for (unsigned l = 0; l < 64; l++) inv_lift(q + (l & 15) + 64 * (l >> 4), 16);
+      for (unsigned l = 0; l < 64; l++) inv_lift(q + (l & 3) + 16 * (l >> 2), 4);
+      for (unsigned l = 0; l < 64; l++) inv_lift(q + 4 * l, 1);
+      break;
   }
 }
 
@@ -225,9 +237,25 @@ static const unsigned char PERM3[64] = {
     37, 40, 34, 10, 7,  19, 28, 13, 49, 52, 41, 38, 26, 23, 29, 53, 11, 35, 44, 14, 50, 56,
     42, 27, 39, 45, 30, 54, 57, 60, 51, 15, 43, 46, 58, 61, 55, 31, 62, 59, 47, 63};
 
+/* libzfp 0.5.5 perm_4 (rodata of /opt/conda/lib/libzfp.so.0.5.5 at 0x4ca00), pinned by the
+ * 4-D libzfp fixtures */
+static const unsigned char PERM4[256] = {
+    0,   1,   4,   16,  64,  5,   80,  17,  68,  65,  20,  2,   8,   32,  128, 84,  81,  69,  21,  6,   18,  66,
+    24,  72,  9,   96,  33,  36,  129, 132, 144, 3,   12,  48,  192, 85,  82,  70,  22,  73,  25,  88,  37,  100,
+    97,  148, 145, 133, 10,  160, 34,  136, 130, 40,  7,   19,  67,  28,  76,  13,  112, 49,  52,  193, 196, 208,
+    86,  89,  101, 149, 161, 137, 41,  134, 38,  164, 26,  152, 146, 104, 98,  74,  83,  71,  23,  77,  29,  92,
+    53,  116, 113, 212, 209, 197, 11,  35,  131, 44,  140, 14,  176, 50,  56,  194, 200, 224, 90,  165, 102, 153,
+    150, 105, 168, 162, 138, 42,  87,  93,  117, 213, 27,  75,  99,  39,  135, 147, 108, 45,  141, 156, 30,  78,
+    177, 180, 54,  114, 120, 57,  198, 210, 216, 201, 225, 228, 15,  240, 51,  204, 195, 60,  169, 166, 154, 106,
+    91,  103, 151, 109, 157, 94,  181, 118, 121, 214, 217, 229, 163, 139, 43,  142, 46,  172, 58,  184, 178, 232,
+    226, 202, 241, 205, 61,  199, 55,  244, 31,  220, 211, 124, 115, 79,  170, 167, 155, 107, 158, 110, 173, 122,
+    185, 182, 233, 230, 218, 95,  245, 119, 221, 215, 125, 242, 206, 62,  203, 59,  248, 47,  236, 227, 188, 179,
+    143, 171, 174, 186, 234, 246, 222, 126, 219, 123, 249, 111, 237, 231, 189, 183, 159, 252, 243, 207, 63,  175,
+    250, 187, 238, 235, 190, 253, 247, 223, 127, 254, 251, 239, 191, 255};
+
 const unsigned char* orc_perm(unsigned dims)
 {
-  return dims == 1 ? PERM1 : dims == 2 ? PERM2 : PERM3;
+  return dims == 1 ? PERM1 : dims == 2 ? PERM2 : dims == 3 ? PERM3 : PERM4;
 }
 
 void orc_fwd_reorder(uint32_t* u, const int32_t* q, unsigned dims)
@@ -238,9 +266,57 @@ void orc_fwd_reorder(uint32_t* u, const int32_t* q, unsigned dims)
   for (unsigned i = 0; i < size; i++) u[i] = ((uint32_t)q[perm[i]] + NBMASK) ^ NBMASK;
 }
 
+/* 256-bit bit planes for 4-D blocks (x[0] holds coefficients 0..63) */
+static uint64_t wide_bits(const uint64_t* x, unsigned o)
+{
+  unsigned i = o >> 6, sh = o & 63;
+  uint64_t v = i < 4 ? x[i] >> sh : 0;
+  if (sh && i + 1 < 4) v |= x[i + 1] << (64 - sh);
+  return v;
+}
+
+static void wide_shr(uint64_t* x, unsigned m)
+{
+  uint64_t y[4];
+  for (unsigned i = 0; i < 4; i++) y[i] = m + 64 * i < 256 ? wide_bits(x, m + 64 * i) : 0;
+  memcpy(x, y, sizeof(y));
+}
+
+static int wide_nonzero(const uint64_t* x) { return (x[0] | x[1] | x[2] | x[3]) != 0; }
+
+/* encode.c:279-339 for 256 coefficients (the same loop, planes of 256 bits) */
+static unsigned encode_ints_256(uint64_t* w, uint64_t* pos, const uint32_t* u, unsigned maxbits, unsigned maxprec)
+{
+  unsigned intprec = 32;
+  unsigned kmin = intprec > maxprec ? intprec - maxprec : 0;
+  unsigned bits = maxbits;
+  unsigned k, m, n;
+  for (k = intprec, n = 0; bits && k-- > kmin;) {
+    uint64_t x[4] = {0, 0, 0, 0};
+    for (unsigned i = 0; i < 256; i++) x[i >> 6] |= (uint64_t)((u[i] >> k) & 1u) << (i & 63);
+    m = OMIN(n, bits);
+    bits -= m;
+    for (unsigned o = 0; o < m; o += 64) put_bits(w, pos, wide_bits(x, o), OMIN(64u, m - o));
+    wide_shr(x, m);
+    for (; bits && n < 256; wide_shr(x, 1), n++) {
+      bits--;
+      if (put_bit(w, pos, (unsigned)wide_nonzero(x))) {
+        for (; bits && n < 255; wide_shr(x, 1), n++) {
+          bits--;
+          if (put_bit(w, pos, (unsigned)(x[0] & 1u))) break;
+        }
+      } else {
+        break;
+      }
+    }
+  }
+  return maxbits - bits;
+}
+
 unsigned orc_encode_ints(uint64_t* w, uint64_t* pos, const uint32_t* u, unsigned maxbits, unsigned maxprec,
                          unsigned size)
 {
+  if (size == 256) return encode_ints_256(w, pos, u, maxbits, maxprec);
   /* encode.c:279-339 (partial) == encode.c:343-408 (all) whenever the budget is not hit */
   unsigned intprec = 32;
   unsigned kmin = intprec > maxprec ? intprec - maxprec : 0;
@@ -273,7 +349,7 @@ unsigned orc_encode_iblock(uint64_t* w, uint64_t* pos, unsigned minbits, unsigne
 {
   /* encode.c:412-455 */
   unsigned size = 1u << (2 * dims);
-  uint32_t u[64];
+  uint32_t u[256];
   orc_fwd_xform(q, dims);
   orc_fwd_reorder(u, q, dims);
   unsigned budget = exceeded_maxbits(maxbits, maxprec, size) ? maxbits : ~0u;
@@ -294,7 +370,7 @@ unsigned orc_encode_fblock(uint64_t* w, uint64_t* pos, const orc_params* p, cons
   unsigned maxprec = orc_precision(emax, p->maxprec, p->minexp, dims);
   unsigned e = maxprec ? (unsigned)(emax + EBIAS) : 0;
   if (e) {
-    int32_t q[64];
+    int32_t q[256];
     bits += EBITS;
     put_bits(w, pos, 2 * (uint64_t)e + 1, bits);
     orc_fwd_cast(q, f, size, emax);
@@ -339,39 +415,45 @@ static void default_strides(unsigned dims, const size_t* n, const ptrdiff_t* s, 
   out[0] = s && s[0] ? s[0] : 1;
   out[1] = s && dims > 1 && s[1] ? s[1] : (ptrdiff_t)n[0];
   out[2] = s && dims > 2 && s[2] ? s[2] : (ptrdiff_t)(n[0] * (dims > 1 ? n[1] : 1));
+  out[3] = s && dims > 3 && s[3] ? s[3] : (ptrdiff_t)(n[0] * (dims > 1 ? n[1] : 1) * (dims > 2 ? n[2] : 1));
 }
 
 void orc_gather_block(float* block, const void* data, int dtype, unsigned dims, const size_t* n,
                       const ptrdiff_t* s, const size_t* b)
 {
-  ptrdiff_t st[3];
+  /* gather_partial_4d_block (encode.c:90-126) generalised: pad each axis in turn */
+  ptrdiff_t st[4];
   default_strides(dims, n, s, st);
-  size_t nv[3] = {1, 1, 1};
+  size_t nv[4] = {1, 1, 1, 1};
   for (unsigned a = 0; a < dims; a++) nv[a] = OMIN((size_t)4, n[a] - 4 * b[a]);
-  unsigned ez = dims > 2 ? 4 : 1, ey = dims > 1 ? 4 : 1;
-  for (unsigned z = 0; z < ez; z++)
-    for (unsigned y = 0; y < ey; y++)
-      for (unsigned x = 0; x < 4; x++) {
-        ptrdiff_t off = (ptrdiff_t)(4 * b[0] + pad_index(x, nv[0])) * st[0];
-        if (dims > 1) off += (ptrdiff_t)(4 * b[1] + pad_index(y, nv[1])) * st[1];
-        if (dims > 2) off += (ptrdiff_t)(4 * b[2] + pad_index(z, nv[2])) * st[2];
-        block[16 * z + 4 * y + x] = load_value(data, dtype, off);
-      }
+  unsigned ew = dims > 3 ? 4 : 1, ez = dims > 2 ? 4 : 1, ey = dims > 1 ? 4 : 1;
+  for (unsigned t = 0; t < ew; t++)
+    for (unsigned z = 0; z < ez; z++)
+      for (unsigned y = 0; y < ey; y++)
+        for (unsigned x = 0; x < 4; x++) {
+          ptrdiff_t off = (ptrdiff_t)(4 * b[0] + pad_index(x, nv[0])) * st[0];
+          if (dims > 1) off += (ptrdiff_t)(4 * b[1] + pad_index(y, nv[1])) * st[1];
+          if (dims > 2) off += (ptrdiff_t)(4 * b[2] + pad_index(z, nv[2])) * st[2];
+          if (dims > 3) off += (ptrdiff_t)(4 * b[3] + pad_index(t, nv[3])) * st[3];
+          block[64 * t + 16 * z + 4 * y + x] = load_value(data, dtype, off);
+        }
 }
 
 static void scatter_block(const float* block, float* data, unsigned dims, const size_t* n, const ptrdiff_t* st,
                           const size_t* b)
 {
-  size_t nv[3] = {1, 1, 1};
+  size_t nv[4] = {1, 1, 1, 1};
   for (unsigned a = 0; a < dims; a++) nv[a] = OMIN((size_t)4, n[a] - 4 * b[a]);
-  for (unsigned z = 0; z < nv[2]; z++)
-    for (unsigned y = 0; y < nv[1]; y++)
-      for (unsigned x = 0; x < nv[0]; x++) {
-        ptrdiff_t off = (ptrdiff_t)(4 * b[0] + x) * st[0];
-        if (dims > 1) off += (ptrdiff_t)(4 * b[1] + y) * st[1];
-        if (dims > 2) off += (ptrdiff_t)(4 * b[2] + z) * st[2];
-        data[off] = block[16 * z + 4 * y + x];
-      }
+  for (unsigned t = 0; t < nv[3]; t++)
+    for (unsigned z = 0; z < nv[2]; z++)
+      for (unsigned y = 0; y < nv[1]; y++)
+        for (unsigned x = 0; x < nv[0]; x++) {
+          ptrdiff_t off = (ptrdiff_t)(4 * b[0] + x) * st[0];
+          if (dims > 1) off += (ptrdiff_t)(4 * b[1] + y) * st[1];
+          if (dims > 2) off += (ptrdiff_t)(4 * b[2] + z) * st[2];
+          if (dims > 3) off += (ptrdiff_t)(4 * b[3] + t) * st[3];
+          data[off] = block[64 * t + 16 * z + 4 * y + x];
+        }
 }
 
 /* ------------------------------------------------------------------------------------------------
@@ -388,17 +470,19 @@ static inline void block_coords(size_t idx, unsigned dims, const size_t* n, size
 {
   size_t bx = (n[0] + 3) / 4;
   size_t by = dims > 1 ? (n[1] + 3) / 4 : 1;
+  size_t bz = dims > 2 ? (n[2] + 3) / 4 : 1;
   b[0] = idx % bx;
   b[1] = (idx / bx) % by;
-  b[2] = idx / (bx * by);
+  b[2] = (idx / (bx * by)) % bz;
+  b[3] = idx / (bx * by * bz);
 }
 
 static uint64_t compress_range(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
                                const orc_params* p, size_t first, size_t last, uint64_t* out)
 {
   uint64_t pos = 0;
-  float f[64];
-  size_t b[3];
+  float f[256];
+  size_t b[4];
   for (size_t i = first; i < last; i++) {
     block_coords(i, dims, n, b);
     orc_gather_block(f, data, dtype, dims, n, s, b);
@@ -497,8 +581,8 @@ void orc_block_bits(const void* data, int dtype, unsigned dims, const size_t* n,
 {
   size_t nb = orc_num_blocks(dims, n);
   uint64_t scratch[300];
-  float f[64];
-  size_t b[3];
+  float f[256];
+  size_t b[4];
   for (size_t i = 0; i < nb; i++) {
     uint64_t pos = 0;
     memset(scratch, 0, sizeof(scratch));
@@ -511,9 +595,31 @@ void orc_block_bits(const void* data, int dtype, unsigned dims, const size_t* n,
 /* ------------------------------------------------------------------------------------------------
  * Decoder (libzfp 0.5.5 semantics; sw/src/decode.c:113-253 with block size 4^d)
  * ---------------------------------------------------------------------------------------------- */
+/* decode.c:141-183 for 256 coefficients */
+static unsigned decode_ints_256(const uint64_t* w, uint64_t* pos, unsigned maxbits, unsigned maxprec, uint32_t* u)
+{
+  unsigned intprec = 32;
+  unsigned kmin = intprec > maxprec ? intprec - maxprec : 0;
+  unsigned bits = maxbits;
+  unsigned i, k, m, n;
+  for (i = 0; i < 256; i++) u[i] = 0;
+  for (k = intprec, n = 0; bits && k-- > kmin;) {
+    m = OMIN(n, bits);
+    bits -= m;
+    uint64_t x[4] = {0, 0, 0, 0};
+    for (unsigned o = 0; o < m; o += 64) x[o >> 6] = get_bits(w, pos, OMIN(64u, m - o));
+    for (; n < 256 && bits && (bits--, get_bit(w, pos)); x[n >> 6] |= (uint64_t)1 << (n & 63), n++)
+      for (; n < 255 && bits && (bits--, !get_bit(w, pos)); n++)
+        ;
+    for (i = 0; i < 256; i++) u[i] += (uint32_t)((x[i >> 6] >> (i & 63)) & 1u) << k;
+  }
+  return maxbits - bits;
+}
+
 static unsigned decode_ints(const uint64_t* w, uint64_t* pos, unsigned maxbits, unsigned maxprec, uint32_t* u,
                             unsigned size)
 {
+  if (size == 256) return decode_ints_256(w, pos, maxbits, maxprec, u);
   /* decode.c:141-183 */
   unsigned intprec = 32;
   unsigned kmin = intprec > maxprec ? intprec - maxprec : 0;
@@ -543,8 +649,8 @@ static unsigned decode_fblock(const uint64_t* w, uint64_t* pos, const orc_params
     unsigned maxprec = orc_precision(emax, p->maxprec, p->minexp, dims);
     unsigned minb = p->minbits - OMIN(bits, p->minbits);
     unsigned maxb = p->maxbits - bits;
-    uint32_t u[64];
-    int32_t q[64];
+    uint32_t u[256];
+    int32_t q[256];
     unsigned budget = exceeded_maxbits(maxb, maxprec, size) ? maxb : ~0u;
     unsigned got = decode_ints(w, pos, budget, maxprec, u, size);
     if (got < minb) {
@@ -571,12 +677,12 @@ uint64_t orc_decompress(float* data, unsigned dims, const size_t* n, const ptrdi
                         const uint64_t* in, size_t in_words)
 {
   (void)in_words;
-  ptrdiff_t st[3];
+  ptrdiff_t st[4];
   default_strides(dims, n, s, st);
   size_t nb = orc_num_blocks(dims, n);
   uint64_t pos = 0;
-  float f[64];
-  size_t b[3];
+  float f[256];
+  size_t b[4];
   for (size_t i = 0; i < nb; i++) {
     block_coords(i, dims, n, b);
     decode_fblock(in, &pos, p, f, dims);
@@ -589,12 +695,12 @@ uint64_t orc_decompress_at(float* data, unsigned dims, const size_t* n, const pt
                            const uint64_t* in, size_t in_words, uint64_t start_bit)
 {
   (void)in_words;
-  ptrdiff_t st[3];
+  ptrdiff_t st[4];
   default_strides(dims, n, s, st);
   size_t nb = orc_num_blocks(dims, n);
   uint64_t pos = start_bit;
-  float f[64];
-  size_t b[3];
+  float f[256];
+  size_t b[4];
   for (size_t i = 0; i < nb; i++) {
     block_coords(i, dims, n, b);
     decode_fblock(in, &pos, p, f, dims);

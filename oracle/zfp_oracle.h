@@ -2,13 +2,13 @@
  * zfp_oracle.h -- TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
  *
  * CPU restatement of the gcow sw/ encoder/decoder (fpgasystems/gcow, sw/src/{encode,decode,stream,common,zfp}.c),
- * generalised to d = 1, 2, 3 exactly as LLNL zfp 0.5.5 does (the library sw/ is byte-identical to).
+ * generalised to d = 1, 2, 3, 4 exactly as LLNL zfp 0.5.5 does (the library sw/ is byte-identical to).
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.
  * The product path (gcow_amd/, libgcow.so) never links or calls it.
  *
  * Parity pins: the reference's own golden streams (the compressed_2d_<n>.zfp files under sw/tests/data and hw/tests/data; via SHA-256
  * manifest in tests/golden/), sw/tests/test_stages.cpp known answers, hw/tests/test_encblock.cpp known answer, the
- * reference sw/ sources compiled into oracle/_ref (2-D), and libzfp 0.5.5 generated fixtures (1-D/3-D/decode).
+ * reference sw/ sources compiled into oracle/_ref (2-D), and libzfp 0.5.5 generated fixtures (1-D/3-D/4-D/decode).
  */
 #ifndef GCOW_ZFP_ORACLE_H
 #define GCOW_ZFP_ORACLE_H
@@ -35,7 +35,7 @@ void orc_fwd_cast(int32_t* iblock, const float* fblock, unsigned n, int emax); /
 void orc_fwd_xform(int32_t* iblock, unsigned dims);                       /* encode.c:189-260 (+1-D/3-D per zfp) */
 void orc_inv_xform(int32_t* iblock, unsigned dims);                       /* decode.c:58-111 (+1-D/3-D) */
 void orc_fwd_reorder(uint32_t* ublock, const int32_t* iblock, unsigned dims); /* encode.c:263-275 */
-const unsigned char* orc_perm(unsigned dims);                             /* types.h:71-97 PERM_2D, identity, PERM_3 */
+const unsigned char* orc_perm(unsigned dims);                             /* types.h:71-97 PERM_2D, identity, PERM_3, PERM_4 */
 /* Embedded bit-plane coder (encode.c:279-408). Appends to a word buffer at bit offset *pos; returns bits written. */
 unsigned orc_encode_ints(uint64_t* words, uint64_t* pos, const uint32_t* ublock, unsigned maxbits,
                          unsigned maxprec, unsigned size);

@@ -127,6 +127,26 @@ def test_libzfp_fixture(orc, fxa, c):
     assert _sha(d.tobytes()) == c["decoded_sha256"]
 
 
+FX4 = load_json("libzfp_fixtures_4d.json")
+
+
+@pytest.fixture(scope="module")
+def fxa4():
+    return np.load(os.path.join(GOLD, "libzfp_fixtures_4d.npz"))
+
+
+@pytest.mark.parametrize("c", FX4["cases"], ids=lambda c: c["name"])
+def test_libzfp_fixture_4d(orc, fxa4, c):
+    """4-D blocks (perm_4, the w-axis lift, 256-bit planes) against libzfp 0.5.5."""
+    a = fxa4["input__" + c["input"]]
+    p = orc.Params(*c["params"])
+    w, bits = orc.compress(a, p)
+    assert w.nbytes == c["bytes"]
+    assert _sha(w.tobytes()) == c["stream_sha256"]
+    d = orc.decompress(fxa4[c["name"] + "__stream"], a.shape, p)
+    assert _sha(d.tobytes()) == c["decoded_sha256"]
+
+
 def test_reference_sw_build_agrees(orc):
     """oracle/_ref: the reference sw/ compiled in place; 2-D expert-param sweep against the restatement."""
     R = orc.ref()
