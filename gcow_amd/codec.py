@@ -51,9 +51,9 @@ def is_fixed(p: GcowParams) -> bool:
 
 # ------------------------------------------------------------------------------------------- fields
 def field_of(t: torch.Tensor, dims: int | None = None) -> ZfpInput:
-    """zfp_input for a 1-3 dim tensor (numpy order: the last axis is x, the fastest)."""
-    if t.dim() < 1 or t.dim() > 3:
-        raise GcowError("tensors of 1-3 dims are supported, got %d" % t.dim())
+    """zfp_input for a 1-4 dim tensor (numpy order: the last axis is x, the fastest)."""
+    if t.dim() < 1 or t.dim() > 4:
+        raise GcowError("tensors of 1-4 dims are supported, got %d" % t.dim())
     if t.dtype == torch.float32:
         dt = DTYPE_FLOAT
     elif t.dtype == torch.bfloat16:
@@ -65,8 +65,8 @@ def field_of(t: torch.Tensor, dims: int | None = None) -> ZfpInput:
     f.data = t.data_ptr()
     shp = list(reversed(t.shape))
     st = list(reversed(t.stride()))
-    names_n = ["nx", "ny", "nz"]
-    names_s = ["sx", "sy", "sz"]
+    names_n = ["nx", "ny", "nz", "nw"]
+    names_s = ["sx", "sy", "sz", "sw"]
     for i in range(t.dim()):
         setattr(f, names_n[i], int(shp[i]))
         setattr(f, names_s[i], int(st[i]))
@@ -85,7 +85,7 @@ def max_output_bytes(shape, p: GcowParams, dtype=torch.float32) -> int:
     f.dtype = DTYPE_FLOAT if dtype == torch.float32 else DTYPE_BF16
     shp = list(reversed(shape))
     for i, n in enumerate(shp):
-        setattr(f, ["nx", "ny", "nz"][i], int(n))
+        setattr(f, ["nx", "ny", "nz", "nw"][i], int(n))
     del t
     return load().gcow_max_output_bytes(C.byref(f), C.byref(p))
 
@@ -164,7 +164,7 @@ def field_of_shape(shape, dtype) -> ZfpInput:
     f = ZfpInput()
     f.dtype = DTYPE_BF16 if dtype == torch.bfloat16 else DTYPE_FLOAT
     for i, n in enumerate(reversed(tuple(shape))):
-        setattr(f, ["nx", "ny", "nz"][i], int(n))
+        setattr(f, ["nx", "ny", "nz", "nw"][i], int(n))
     return f
 
 

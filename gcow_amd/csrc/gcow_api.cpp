@@ -72,7 +72,7 @@ gcow_status make_field(const zfp_input* in, gcow::FieldDesc& F, bool for_decode)
   if (!in) return fail(GCOW_ERR_INVALID, "null field");
   const uint32_t d = dims_of(in);
   if (d == 0) return fail(GCOW_ERR_INVALID, "field has no extents");
-  if (d > 3) return fail(GCOW_ERR_UNSUPPORTED, "4-D fields are not supported");
+
   if (for_decode) {
     if (in->dtype != dtype_float) return fail(GCOW_ERR_UNSUPPORTED, "decode writes fp32 (dtype_float) only");
   } else if (in->dtype != dtype_float && in->dtype != dtype_bf16) {
@@ -85,19 +85,23 @@ gcow_status make_field(const zfp_input* in, gcow::FieldDesc& F, bool for_decode)
   F.n[0] = in->nx;
   F.n[1] = d > 1 ? in->ny : 1;
   F.n[2] = d > 2 ? in->nz : 1;
+  F.n[3] = d > 3 ? in->nw : 1;
   F.s[0] = in->sx ? in->sx : 1;
   F.s[1] = d > 1 ? (in->sy ? in->sy : (ptrdiff_t)in->nx) : 0;
   F.s[2] = d > 2 ? (in->sz ? in->sz : (ptrdiff_t)(in->nx * in->ny)) : 0;
-  const uint64_t bx = (F.n[0] + 3) / 4, by = (F.n[1] + 3) / 4, bz = (F.n[2] + 3) / 4;
-  const uint64_t nb = bx * by * bz;
+  F.s[3] = d > 3 ? (in->sw ? in->sw : (ptrdiff_t)(in->nx * in->ny * in->nz)) : 0;
+  const uint64_t bx = (F.n[0] + 3) / 4, by = (F.n[1] + 3) / 4, bz = (F.n[2] + 3) / 4, bw = (F.n[3] + 3) / 4;
+  const uint64_t nb = bx * by * bz * bw;
   if (nb >= (1ull << 32) || bx >= (1ull << 32)) return fail(GCOW_ERR_UNSUPPORTED, "more than 2^32 blocks per call");
   F.bx = (uint32_t)bx;
   F.by = (uint32_t)by;
   F.bz = (uint32_t)bz;
+  F.bw = (uint32_t)bw;
   F.nblocks = (uint32_t)nb;
   const size_t esz = F.dtype == gcow::DT_BF16 ? 2 : 4;
   const bool aligned = ((uintptr_t)in->data % (4 * esz)) == 0;
-  F.vec = (F.s[0] == 1 && aligned && (d < 2 || F.s[1] % 4 == 0) && (d < 3 || F.s[2] % 4 == 0)) ? 1u : 0u;
+  F.vec = (F.s[0] == 1 && aligned && (d < 2 || F.s[1] % 4 == 0) && (d < 3 || F.s[2] % 4 == 0) &&
+           (d < 4 || F.s[3] % 4 == 0)) ? 1u : 0u;
   return GCOW_OK;
 }
 
@@ -164,6 +168,23 @@ gcow_status encode_impl(const zfp_input* field, const gcow_params* p, void* d_ou
     return GCOW_OK;
   }
   const gcow::Params pp = P(*p);
+  if (F.dims == 4) {  // one wave per 256-value block
+    if (p->minbits == p->maxbits) {
+      if (p->maxbits % 32) GCOW_HIP(hipMemsetAsync(d_out, 0, bound, (hipStream_t)stream));  // shared boundary words
+      GCOW_HIP(gcow::launch_encode4d(F, pp, nullptr, nullptr, (uint32_t*)d_out, d_index, shift, stream));
+      if (d_total_bits) GCOW_HIP(gcow::launch_set_u64(d_total_bits, (uint64_t)F.nblocks * p->maxbits, stream));
+      return GCOW_OK;
+    }
+    const size_t need = gcow_encode_workspace_bytes(field, p);
+    if (!d_ws || ws_bytes < need) return fail(GCOW_ERR_INVALID, "workspace smaller than gcow_encode_workspace_bytes()");
+    uint64_t* sums = (uint64_t*)d_ws;
+    uint64_t* base = sums + F.nblocks;
+    uint32_t* lens = (uint32_t*)(base + F.nblocks + 1);
+    GCOW_HIP(gcow::launch_encode4d(F, pp, lens, nullptr, nullptr, nullptr, 0, stream));
+    GCOW_HIP(gcow::launch_scan_blocks(lens, F.nblocks, sums, base, d_total_bits, (uint32_t*)d_out, stream));
+    GCOW_HIP(gcow::launch_encode4d(F, pp, nullptr, base, (uint32_t*)d_out, d_index, shift, stream));
+    return GCOW_OK;
+  }
   if (fast1d_ok(F, *p, d_index)) {
     GCOW_HIP(gcow::launch_encode_fixed1d(F.data, (int)F.dtype, F.n[0], F.nblocks, pp, d_out, stream));
     if (p->maxbits == 32 && (F.nblocks & 1))  // stream_flush: zero the upper half of the last word
@@ -205,6 +226,12 @@ gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void
   if (fixed && F.dims == 1 && F.vec && (p->maxbits == 64 || p->maxbits == 32) && p->maxprec >= 32 &&
       p->minexp <= -154 && base_bits % 32 == 0 && !d_end && !getenv("GCOW_GENERIC_DECODE")) {
     GCOW_HIP(gcow::launch_decode_fixed1d(F, P(*p), (const uint64_t*)d_in, base_bits, stream));
+    return GCOW_OK;
+  }
+  if (F.dims == 4) {
+    if (!fixed && (!d_index || index_stride != 1))
+      return fail(GCOW_ERR_UNSUPPORTED, "4-D variable-rate decode needs the block index with index_stride 1");
+    GCOW_HIP(gcow::launch_decode4d(F, P(*p), (const uint64_t*)d_in, fixed ? nullptr : d_index, base_bits, stream));
     return GCOW_OK;
   }
   if (fixed && F.dims == 3 && base_bits % 32 == 0 && !d_end && gcow::fixed3d_ok(p->maxbits)) {
@@ -691,7 +718,7 @@ size_t stream_algin_next_word(stream* s)
 size_t gcow_max_output_bytes(const zfp_input* field, const gcow_params* p)
 {
   const uint32_t d = dims_of(field);
-  if (!d || d > 3 || !p) return 0;
+  if (!d || d > 4 || !p) return 0;
   const uint64_t nb = get_input_num_blocks(field);
   return (size_t)((nb * block_bits_bound(*p, d) + 63) / 64 * 8 + 8);
 }
@@ -700,6 +727,7 @@ size_t gcow_encode_workspace_bytes(const zfp_input* field, const gcow_params* p)
 {
   gcow::FieldDesc F;
   if (make_field(field, F, false) || !p || p->minbits == p->maxbits) return 0;
+  if (F.dims == 4) return (size_t)F.nblocks * 4 + (2 * (size_t)F.nblocks + 1) * 8 + 16;  // lens, sums, base
   const gcow::TilePlan pl = make_plan(F, *p);
   return (2 * (size_t)pl.nranges + 1) * 8;
 }

@@ -1108,6 +1108,293 @@ __global__ __launch_bounds__(256) void k_decode3d_fixed(FieldDesc F, Params p, c
   }
 }
 
+// ------------------------------------------------------------------------------------------------ 4-D blocks
+// sw/ declares the 4-D gather (gather_partial_4d_block, sw/src/encode.c:90-126) and zfp_input's
+// nw / sw (sw/include/types.h:51-56) but never codes 4-D; libzfp 0.5.5 does, with perm_4 and x, y, z, w lifts.
+// One wave per 256-value block: lane l holds the x-row (y, z, w) = (l & 3, (l >> 2) & 3, l >> 4); the lifts run over
+// LDS lines (one line per lane per direction); the bit planes are wave ballots (word j = coefficients 64j .. 64j+63,
+// lane l owning coefficients l + 64j); the embedded coder runs wave-uniformly on the 256-bit planes with a
+// count-trailing-zeros group-test scan, and lane 0 writes the bits into the block's LDS bit buffer.
+__device__ const uint8_t g_perm4[256] = {
+    0,   1,   4,   16,  64,  5,   80,  17,  68,  65,  20,  2,   8,   32,  128, 84,  81,  69,  21,  6,   18,  66,
+    24,  72,  9,   96,  33,  36,  129, 132, 144, 3,   12,  48,  192, 85,  82,  70,  22,  73,  25,  88,  37,  100,
+    97,  148, 145, 133, 10,  160, 34,  136, 130, 40,  7,   19,  67,  28,  76,  13,  112, 49,  52,  193, 196, 208,
+    86,  89,  101, 149, 161, 137, 41,  134, 38,  164, 26,  152, 146, 104, 98,  74,  83,  71,  23,  77,  29,  92,
+    53,  116, 113, 212, 209, 197, 11,  35,  131, 44,  140, 14,  176, 50,  56,  194, 200, 224, 90,  165, 102, 153,
+    150, 105, 168, 162, 138, 42,  87,  93,  117, 213, 27,  75,  99,  39,  135, 147, 108, 45,  141, 156, 30,  78,
+    177, 180, 54,  114, 120, 57,  198, 210, 216, 201, 225, 228, 15,  240, 51,  204, 195, 60,  169, 166, 154, 106,
+    91,  103, 151, 109, 157, 94,  181, 118, 121, 214, 217, 229, 163, 139, 43,  142, 46,  172, 58,  184, 178, 232,
+    226, 202, 241, 205, 61,  199, 55,  244, 31,  220, 211, 124, 115, 79,  170, 167, 155, 107, 158, 110, 173, 122,
+    185, 182, 233, 230, 218, 95,  245, 119, 221, 215, 125, 242, 206, 62,  203, 59,  248, 47,  236, 227, 188, 179,
+    143, 171, 174, 186, 234, 246, 222, 126, 219, 123, 249, 111, 237, 231, 189, 183, 159, 252, 243, 207, 63,  175,
+    250, 187, 238, 235, 190, 253, 247, 223, 127, 254, 251, 239, 191, 255};
+
+struct Plane256 {
+  uint64_t w[4];
+  __device__ __forceinline__ uint64_t bits(uint32_t o) const  // 64 bits from bit o (zeros past 256)
+  {
+    const uint32_t i = o >> 6, sh = o & 63;
+    uint64_t v = i < 4 ? w[i] >> sh : 0ull;
+    if (sh && i + 1 < 4) v |= w[i + 1] << (64 - sh);
+    return v;
+  }
+  __device__ __forceinline__ void shr(uint32_t m)
+  {
+    uint64_t y[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) y[i] = m + 64u * i < 256u ? bits(m + 64u * i) : 0ull;
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[i] = y[i];
+  }
+  __device__ __forceinline__ uint32_t ctz() const  // 256 when zero
+  {
+    return w[0] ? __builtin_ctzll(w[0]) : w[1] ? 64 + __builtin_ctzll(w[1]) : w[2] ? 128 + __builtin_ctzll(w[2])
+           : w[3] ? 192 + __builtin_ctzll(w[3]) : 256u;
+  }
+};
+
+// Wave-uniform writer into a zeroed LDS bit buffer; lane 0 stores. Bits past `limit` are dropped.
+struct UniWriter {
+  uint32_t* buf;
+  uint32_t pos, limit, lane;
+  __device__ __forceinline__ void put(uint64_t v, uint32_t n)
+  {
+    if (pos < limit && n) {
+      const uint32_t k = min(n, limit - pos);
+      v &= lowmask64(k);
+      if (lane == 0) {
+        const uint32_t i = pos >> 5, sh = pos & 31;
+        buf[i] |= (uint32_t)(v << sh);
+        const uint64_t r = sh ? v >> (32 - sh) : v >> 32;
+        if (k + sh > 32) buf[i + 1] |= (uint32_t)r;
+        if (k + sh > 64) buf[i + 2] |= (uint32_t)(r >> 32);
+      }
+    }
+    pos += n;
+  }
+  __device__ __forceinline__ void skip(uint32_t n) { pos += n; }
+};
+
+__device__ __forceinline__ void block4d_coords(const FieldDesc& F, uint32_t b, uint32_t* ib)
+{
+  uint32_t r = b / F.bx;
+  ib[0] = b - r * F.bx;
+  uint32_t r2 = r / F.by;
+  ib[1] = r - r2 * F.by;
+  ib[3] = r2 / F.bz;
+  ib[2] = r2 - ib[3] * F.bz;
+}
+
+// LDS line lifts of a 4 x 4 x 4 x 4 int block, one line per lane, in libzfp's direction order
+__device__ __forceinline__ void lift4d_lines(int32_t* q, uint32_t lane, bool inverse)
+{
+#pragma unroll
+  for (int step = 0; step < 4; step++) {
+    const int dir = inverse ? 3 - step : step;
+    uint32_t base, st;
+    if (dir == 0) { base = 4 * lane; st = 1; }
+    else if (dir == 1) { base = (lane & 3) + 16 * (lane >> 2); st = 4; }
+    else if (dir == 2) { base = (lane & 15) + 64 * (lane >> 4); st = 16; }
+    else { base = lane; st = 64; }
+    int32_t x = q[base], y = q[base + st], z = q[base + 2 * st], w = q[base + 3 * st];
+    if (inverse) inv_lift(x, y, z, w);
+    else fwd_lift(x, y, z, w);
+    q[base] = x; q[base + st] = y; q[base + 2 * st] = z; q[base + 3 * st] = w;
+    __syncthreads();
+  }
+}
+
+// encode: lens != null -> bit count per block; else write at rbase[b] (variable) or b * maxbits (fixed)
+template <int DT>
+__global__ __launch_bounds__(64) void k_encode4d(FieldDesc F, Params p, uint32_t* __restrict__ lens,
+                                                 const uint64_t* __restrict__ rbase, uint32_t* __restrict__ out32,
+                                                 uint64_t* __restrict__ index, uint32_t index_shift)
+{
+  constexpr uint32_t OBW = (31 + 9 + 255 + 256 * 32 + 16658 + 31) / 32 + 3;  // header + bound (+ pad to minbits)
+  __shared__ int32_t q[256];
+  __shared__ uint32_t obuf[OBW];
+  const uint32_t lane = threadIdx.x, b = blockIdx.x;
+  uint32_t ib[4];
+  block4d_coords(F, b, ib);
+  uint32_t nv[4];
+#pragma unroll
+  for (int a = 0; a < 4; a++) nv[a] = (uint32_t)min<uint64_t>(4, F.n[a] - 4ull * ib[a]);
+  const uint32_t y = lane & 3, z = (lane >> 2) & 3, t = lane >> 4;
+  const int64_t row = (int64_t)(4ull * ib[1] + pad_index(y, nv[1])) * F.s[1] +
+                      (int64_t)(4ull * ib[2] + pad_index(z, nv[2])) * F.s[2] +
+                      (int64_t)(4ull * ib[3] + pad_index(t, nv[3])) * F.s[3] + (int64_t)(4ull * ib[0]) * F.s[0];
+  float f[4];
+#pragma unroll
+  for (int x = 0; x < 4; x++) f[x] = load_elem<DT>(F.data, row + (int64_t)pad_index(x, nv[0]) * F.s[0]);
+  uint32_t m = 0;
+#pragma unroll
+  for (int x = 0; x < 4; x++) {
+    const uint32_t a = __float_as_uint(f[x]) & 0x7fffffffu;
+    m = (a <= 0x7f800000u && a > m) ? a : m;  // NaN never wins (encode.c:146-150)
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+  const int emax = m == 0 ? -127 : (m >= 0x7f800000u ? 0 : max((int)(m >> 23) - 126, -126));
+  const uint32_t prec = precision(emax, p.maxprec, p.minexp, 4);
+  const uint32_t be = prec ? (uint32_t)(emax + 127) : 0u;
+  const uint32_t o0 = lens ? 0u : (uint32_t)((rbase ? rbase[b] : (uint64_t)b * p.maxbits) & 31u);
+  for (uint32_t i = lane; i < OBW; i += 64) obuf[i] = 0u;
+  __syncthreads();
+  UniWriter w{obuf, o0, o0 + p.maxbits, lane};
+  uint32_t total;
+  if (!be) {
+    total = max(1u, p.minbits);
+  } else {
+    w.put(2ull * be + 1ull, 9);
+    const float sc = cast_scale(emax);
+    int32_t qq[4];
+#pragma unroll
+    for (int x = 0; x < 4; x++) qq[x] = cast1(f[x], sc);
+#pragma unroll
+    for (int x = 0; x < 4; x++) q[4 * lane + x] = qq[x];
+    __syncthreads();
+    lift4d_lines(q, lane, false);
+    uint32_t u[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) u[j] = ((uint32_t)q[g_perm4[lane + 64 * j]] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+    const uint32_t maxb = p.maxbits - 9u, minb = p.minbits - min(p.minbits, 9u);
+    const uint32_t budget = exceeded_maxbits(maxb, prec, 256) ? maxb : 0xffffffffu;
+    const int kmin = prec < 32 ? 32 - (int)prec : 0;
+    uint32_t bits = 0, n = 0;  // encode_partial_bitplanes (encode.c:279-339), planes of 256 bits
+    for (int k = 31; k >= kmin && bits < budget; --k) {
+      Plane256 x;
+#pragma unroll
+      for (int j = 0; j < 4; j++) x.w[j] = __ballot((u[j] >> k) & 1u);
+      for (uint32_t o = 0; o < n; o += 64) w.put(x.bits(o) & lowmask64(min(64u, n - o)), min(64u, n - o));
+      bits += n;
+      x.shr(n);
+      while (n < 256 && bits < budget) {
+        const uint32_t tz = x.ctz();
+        if (tz == 256) {  // negative group test
+          w.skip(1);
+          bits += 1;
+          break;
+        }
+        if (n + tz < 255) {  // group '1', tz zeros, the one-bit
+          w.put(1ull, 1);
+          w.skip(tz);
+          w.put(1ull, 1);
+          bits += tz + 2;
+          n += tz + 1;
+          x.shr(tz + 1);
+        } else {  // the one-bit sits in the last position and is implied
+          w.put(1ull, 1);
+          w.skip(255 - n);
+          bits += 256 - n;
+          n = 256;
+        }
+      }
+    }
+    bits = bits < budget ? bits : budget;
+    total = 9 + max(bits, minb);
+  }
+  if (lens) {
+    if (lane == 0) lens[b] = total;
+    return;
+  }
+  __syncthreads();
+  const uint64_t base = rbase ? rbase[b] : (uint64_t)b * p.maxbits;
+  const uint32_t W = (o0 + total + 31) >> 5;
+  const uint64_t gw0 = base >> 5;
+  for (uint32_t j = lane; j < W; j += 64) {
+    const uint32_t v = obuf[j];
+    if ((j == 0 && o0) || (j == W - 1 && ((o0 + total) & 31))) atomicOr(out32 + gw0 + j, v);  // shared words
+    else out32[gw0 + j] = v;
+  }
+  if (index && lane == 0 && (b & ((1u << index_shift) - 1)) == 0) index[b >> index_shift] = base;
+  if (lane == 0 && b == F.nblocks - 1) {
+    const uint64_t endw = (base + total + 31) >> 5;
+    if (endw & 1) out32[endw] = 0u;  // stream_flush: zero-pad to a 64-bit boundary
+  }
+}
+
+// decode: blocks at index[b] (variable, index stride 1) or b * maxbits (fixed), libzfp decode_ints semantics
+__global__ __launch_bounds__(64) void k_decode4d(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                 const uint64_t* __restrict__ index, uint64_t base_bits)
+{
+  __shared__ int32_t q[256];
+  const uint32_t lane = threadIdx.x, b = blockIdx.x;
+  BitReader r{in, base_bits + (index ? index[b] : (uint64_t)b * p.maxbits)};
+  uint32_t u[4] = {0u, 0u, 0u, 0u};
+  int emax = 0;
+  const bool nonzero = r.bit();
+  if (nonzero) {
+    emax = (int)r.get(8) - 127;
+    const uint32_t prec = precision(emax, p.maxprec, p.minexp, 4);
+    const uint32_t maxb = p.maxbits - 9u;
+    uint32_t bits = exceeded_maxbits(maxb, prec, 256) ? maxb : 0xffffffffu;
+    const int kmin = prec < 32 ? 32 - (int)prec : 0;
+    uint32_t n = 0;
+    for (int k = 31; bits && k >= kmin; --k) {  // decode.c:141-183 with 256-bit planes
+      Plane256 x{{0ull, 0ull, 0ull, 0ull}};
+      const uint32_t m = min(n, bits);
+      bits -= m;
+      for (uint32_t o = 0; o < m; o += 64) x.w[o >> 6] = r.get(min(64u, m - o));
+      while (n < 256 && bits) {
+        bits--;
+        if (!r.bit()) break;  // negative group test
+        uint32_t lim = min(255u - n, bits), adv = 0;  // zeros the scan may read
+        for (;;) {
+          const uint64_t v = r.peek64();
+          const uint32_t zz = v ? (uint32_t)__builtin_ctzll(v) : 64u;
+          if (adv + zz < lim && zz < 64) {  // zeros, then the one-bit
+            r.pos += zz + 1;
+            bits -= zz + 1;
+            n += zz;
+            adv = 0xffffffffu;
+            break;
+          }
+          if (zz == 64 && adv + 64 < lim) {
+            r.pos += 64;
+            bits -= 64;
+            n += 64;
+            adv += 64;
+            continue;
+          }
+          r.pos += lim - adv;  // the scan ran into the last coefficient or the budget: the one is implied
+          bits -= lim - adv;
+          n += lim - adv;
+          break;
+        }
+        x.w[n >> 6] |= 1ull << (n & 63);
+        n++;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) u[j] |= (uint32_t)((x.w[j] >> lane) & 1u) << k;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) q[g_perm4[lane + 64 * j]] = (int32_t)((u[j] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+  __syncthreads();
+  lift4d_lines(q, lane, true);
+  const float sc = dequant_scale(emax);
+  uint32_t ib[4];
+  block4d_coords(F, b, ib);
+  uint32_t nv[4];
+#pragma unroll
+  for (int a = 0; a < 4; a++) nv[a] = (uint32_t)min<uint64_t>(4, F.n[a] - 4ull * ib[a]);
+  const uint32_t y = lane & 3, z = (lane >> 2) & 3, t = lane >> 4;
+  if (y < nv[1] && z < nv[2] && t < nv[3]) {
+    float* out = (float*)F.data;
+    const int64_t row = (int64_t)(4ull * ib[0]) * F.s[0] + (int64_t)(4ull * ib[1] + y) * F.s[1] +
+                        (int64_t)(4ull * ib[2] + z) * F.s[2] + (int64_t)(4ull * ib[3] + t) * F.s[3];
+    for (uint32_t x = 0; x < nv[0]; x++) out[row + (int64_t)x * F.s[0]] = nonzero ? sc * (float)q[4 * lane + x] : 0.0f;
+  }
+}
+
+// exclusive scan of per-block lengths: one "range" per block through k_scan_ranges (which also zeroes the words
+// two blocks share)
+__global__ void k_widen_u32(const uint32_t* __restrict__ a, uint32_t n, uint64_t* __restrict__ o)
+{
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i < n) o[i] = a[i];
+}
+
 // ------------------------------------------------------------------------------------------------ decode
 template <int D>
 __global__ __launch_bounds__(64) void k_decode(FieldDesc F, Params p, const uint64_t* __restrict__ in,
@@ -1976,6 +2263,31 @@ hipError_t launch_decode3d_fixed(const FieldDesc& F, const Params& p, const uint
     case 64: return launch_dec3d_t<64>(F, p, in32, st);
   }
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_encode4d(const FieldDesc& F, const Params& p, uint32_t* lens, const uint64_t* rbase, uint32_t* out32,
+                           uint64_t* index, uint32_t index_shift, void* stream)
+{
+  if (F.dtype == DT_BF16)
+    k_encode4d<DT_BF16><<<F.nblocks, 64, 0, S(stream)>>>(F, p, lens, rbase, out32, index, index_shift);
+  else
+    k_encode4d<DT_F32><<<F.nblocks, 64, 0, S(stream)>>>(F, p, lens, rbase, out32, index, index_shift);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode4d(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
+                           uint64_t base_bits, void* stream)
+{
+  k_decode4d<<<F.nblocks, 64, 0, S(stream)>>>(F, p, in, index, base_bits);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_blocks(const uint32_t* lens, uint32_t nblocks, uint64_t* sums, uint64_t* base, uint64_t* total,
+                              uint32_t* out32, void* stream)
+{
+  k_widen_u32<<<(nblocks + 255) / 256, 256, 0, S(stream)>>>(lens, nblocks, sums);
+  k_scan_ranges<<<1, 1024, 0, S(stream)>>>(sums, nblocks, base, total, out32, nullptr);
+  return hipGetLastError();
 }
 
 hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t in_words,

@@ -11,9 +11,9 @@ namespace gcow {
 // Field geometry as the kernels see it: extents/strides fastest-first, unused dims have extent 1.
 struct FieldDesc {
   const void* data;  // input (encode) or output (decode) device pointer
-  uint64_t n[3];
-  int64_t s[3];
-  uint32_t bx, by, bz;
+  uint64_t n[4];
+  int64_t s[4];
+  uint32_t bx, by, bz, bw;
   uint32_t nblocks;
   uint32_t dims;
   uint32_t dtype;
@@ -51,6 +51,13 @@ hipError_t launch_decode3d_fixed(const FieldDesc& F, const Params& p, const uint
 hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t in_words,
                                const uint64_t* index, uint32_t chunk, uint64_t nchunks, uint64_t base_bits,
                                uint64_t* end_out, void* stream);
+// 4-D blocks (one wave per block): lens (count pass), or write at rbase (variable) / b * maxbits (fixed, rbase null)
+hipError_t launch_encode4d(const FieldDesc& F, const Params& p, uint32_t* lens, const uint64_t* rbase, uint32_t* out32,
+                           uint64_t* index, uint32_t index_shift, void* stream);
+hipError_t launch_decode4d(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
+                           uint64_t base_bits, void* stream);
+hipError_t launch_scan_blocks(const uint32_t* lens, uint32_t nblocks, uint64_t* sums, uint64_t* base, uint64_t* total,
+                              uint32_t* out32, void* stream);
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
 hipError_t launch_prepend_header(uint64_t* dst, uint32_t off, const uint64_t* src, const uint64_t* d_bits,
                                  const uint64_t* header, uint64_t max_words, uint64_t* d_total, void* stream);

@@ -635,3 +635,34 @@ def test_staged_decode_wide_blocks(gc, orc, shape):
     stride = 16 if len(shape) == 1 else 1
     _check_vs_oracle(gc, orc, a, orc.precision(32), index_stride=stride)
     _check_vs_oracle(gc, orc, a, orc.accuracy(1e-30), index_stride=stride)
+
+
+FX4 = json.load(open(os.path.join(GOLD, "libzfp_fixtures_4d.json")))["cases"]
+
+
+@pytest.fixture(scope="module")
+def fxa4():
+    return np.load(os.path.join(GOLD, "libzfp_fixtures_4d.npz"))
+
+
+@pytest.mark.parametrize("c", FX4, ids=lambda c: c["name"])
+def test_libzfp_fixture_4d_device(gc, fxa4, c):
+    """4-D blocks on the GPU (one wave per block) against libzfp 0.5.5: stream bytes and decoded values."""
+    a = fxa4["input__" + c["input"]]
+    p = gc.expert(*c["params"])
+    e, b = dev_encode_bytes(gc, a, p, index_stride=0 if gc.is_fixed(p) else 1)
+    assert len(b) == c["bytes"]
+    assert _sha(b) == c["stream_sha256"]
+    d = gc.decode(e)
+    torch.cuda.synchronize()
+    assert _sha(d.cpu().numpy().tobytes()) == c["decoded_sha256"]
+
+
+def test_4d_random_and_bf16(gc, orc):
+    """4-D random fields (partial blocks on every axis) and a bf16 input vs the oracle."""
+    rng = np.random.default_rng(44)
+    a = (rng.standard_normal((6, 5, 7, 10)) * 1e-2).astype(np.float32)
+    for op in (orc.rate(8, 4), orc.accuracy(1e-4), orc.precision(20)):
+        _check_vs_oracle(gc, orc, a, op, index_stride=0 if op.minbits == op.maxbits else 1)
+    bf = (a.view(np.uint32) >> 16).astype(np.uint16)
+    _check_vs_oracle(gc, orc, bf, orc.accuracy(1e-3), index_stride=1, decode=False)
