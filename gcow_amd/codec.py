@@ -169,7 +169,7 @@ def field_of_shape(shape, dtype) -> ZfpInput:
 
 
 def encode(x: torch.Tensor, params: GcowParams, index_stride: int = 0, stream=None) -> Encoded:
-    """zfp_compress of a device tensor (1-3 dims, fp32 or bf16, any strides)."""
+    """zfp_compress of a device tensor (1-4 dims, fp32 or bf16, any strides)."""
     if not x.is_cuda:
         raise GcowError("encode expects a device tensor (use gcow_amd.dropin for host arrays)")
     enc = Encoder(x.shape, x.dtype, params, x.device, index_stride)
@@ -240,7 +240,7 @@ def read_header(words):
     bits = load().gcow_read_header(arr, 3, C.byref(f), C.byref(p))
     if not bits:
         raise GcowError("not a zfp 0.5.5 float stream (bad magic, version or type)")
-    shape = tuple(n for n in (f.nz, f.ny, f.nx) if n)
+    shape = tuple(n for n in (f.nw, f.nz, f.ny, f.nx) if n)
     return shape, p, int(bits)
 
 

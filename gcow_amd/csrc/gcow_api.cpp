@@ -228,10 +228,11 @@ gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void
     GCOW_HIP(gcow::launch_decode_fixed1d(F, P(*p), (const uint64_t*)d_in, base_bits, stream));
     return GCOW_OK;
   }
-  if (F.dims == 4) {
-    if (!fixed && (!d_index || index_stride != 1))
-      return fail(GCOW_ERR_UNSUPPORTED, "4-D variable-rate decode needs the block index with index_stride 1");
-    GCOW_HIP(gcow::launch_decode4d(F, P(*p), (const uint64_t*)d_in, fixed ? nullptr : d_index, base_bits, stream));
+  if (F.dims == 4) {  // one wave per block; a variable-rate stream without a stride-1 index is walked in order
+    if ((!fixed && (!d_index || index_stride != 1)) || d_end)
+      GCOW_HIP(gcow::launch_decode4d_seq(F, P(*p), (const uint64_t*)d_in, base_bits, d_end, stream));
+    else
+      GCOW_HIP(gcow::launch_decode4d(F, P(*p), (const uint64_t*)d_in, fixed ? nullptr : d_index, base_bits, stream));
     return GCOW_OK;
   }
   if (fixed && F.dims == 3 && base_bits % 32 == 0 && !d_end && gcow::fixed3d_ok(p->maxbits)) {
@@ -814,9 +815,9 @@ uint gcow_header_bits(const gcow_params* p) { return p && hdr_mode(*p) < 0xfffu 
 uint gcow_write_header(const zfp_input* field, const gcow_params* p, uint64_t* words)
 {
   const uint32_t d = dims_of(field);
-  if (!p || !words || d < 1 || d > 3) return 0;
-  const size_t n[3] = {field->nx, field->ny, field->nz};
-  const uint32_t w = d == 1 ? 48 : d == 2 ? 24 : 16;
+  if (!p || !words || d < 1 || d > 4) return 0;
+  const size_t n[4] = {field->nx, field->ny, field->nz, field->nw};
+  const uint32_t w = d == 1 ? 48 : d == 2 ? 24 : d == 3 ? 16 : 12;
   for (uint32_t a = 0; a < d; a++)
     if (n[a] == 0 || (w < 64 && (uint64_t)(n[a] - 1) >> w)) return 0;
   uint64_t meta = 0;
@@ -843,9 +844,8 @@ uint gcow_read_header(const uint64_t* words, size_t nwords, zfp_input* field, gc
   meta >>= 2;
   const uint32_t d = (uint32_t)(meta & 3u) + 1;
   meta >>= 2;
-  if (d > 3) return 0;
-  const uint32_t bw = d == 1 ? 48 : d == 2 ? 24 : 16;
-  size_t n[3] = {0, 0, 0};
+  const uint32_t bw = d == 1 ? 48 : d == 2 ? 24 : d == 3 ? 16 : 12;
+  size_t n[4] = {0, 0, 0, 0};
   for (uint32_t a = 0; a < d; a++) {
     n[a] = (size_t)(meta & ((1ull << bw) - 1)) + 1;
     meta >>= bw;
@@ -875,7 +875,7 @@ uint gcow_read_header(const uint64_t* words, size_t nwords, zfp_input* field, gc
   field->nx = n[0];
   field->ny = n[1];
   field->nz = n[2];
-  field->nw = 0;
+  field->nw = n[3];
   *p = q;
   return pos;
 }
@@ -893,7 +893,7 @@ gcow_status gcow_encode_device_zfp(const zfp_input* field, const gcow_params* p,
 {
   uint64_t h[3];
   const uint32_t hb = gcow_write_header(field, p, h);
-  if (!hb) return fail(GCOW_ERR_INVALID, "field shape not representable in a zfp header (dims 1-3)");
+  if (!hb) return fail(GCOW_ERR_INVALID, "field shape not representable in a zfp header (dims 1-4, 12 bits per axis in 4-D)");
   const size_t bound = gcow_max_output_bytes(field, p);
   if (!d_out || out_capacity < bound + 24) return fail(GCOW_ERR_CAPACITY, "output capacity below bound + 24");
   if (!d_workspace || workspace_bytes < gcow_encode_zfp_workspace_bytes(field, p))

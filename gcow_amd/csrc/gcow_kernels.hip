@@ -1313,13 +1313,12 @@ __global__ __launch_bounds__(64) void k_encode4d(FieldDesc F, Params p, uint32_t
   }
 }
 
-// decode: blocks at index[b] (variable, index stride 1) or b * maxbits (fixed), libzfp decode_ints semantics
-__global__ __launch_bounds__(64) void k_decode4d(FieldDesc F, Params p, const uint64_t* __restrict__ in,
-                                                 const uint64_t* __restrict__ index, uint64_t base_bits)
+// decode one 4-D block at r.pos (wave-uniform reads; every lane ends with the same r.pos), then scatter it;
+// libzfp decode_ints semantics. Returns the bits the block occupies in a variable-rate stream (padded to minbits).
+__device__ __forceinline__ uint64_t decode4d_block(const FieldDesc& F, const Params& p, BitReader& r, uint32_t b,
+                                                   int32_t* q, uint32_t lane)
 {
-  __shared__ int32_t q[256];
-  const uint32_t lane = threadIdx.x, b = blockIdx.x;
-  BitReader r{in, base_bits + (index ? index[b] : (uint64_t)b * p.maxbits)};
+  const uint64_t start = r.pos;
   uint32_t u[4] = {0u, 0u, 0u, 0u};
   int emax = 0;
   const bool nonzero = r.bit();
@@ -1346,7 +1345,6 @@ __global__ __launch_bounds__(64) void k_decode4d(FieldDesc F, Params p, const ui
             r.pos += zz + 1;
             bits -= zz + 1;
             n += zz;
-            adv = 0xffffffffu;
             break;
           }
           if (zz == 64 && adv + 64 < lim) {
@@ -1368,6 +1366,7 @@ __global__ __launch_bounds__(64) void k_decode4d(FieldDesc F, Params p, const ui
       for (int j = 0; j < 4; j++) u[j] |= (uint32_t)((x.w[j] >> lane) & 1u) << k;
     }
   }
+  const uint64_t used = max<uint64_t>(r.pos - start, p.minbits);
 #pragma unroll
   for (int j = 0; j < 4; j++) q[g_perm4[lane + 64 * j]] = (int32_t)((u[j] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
   __syncthreads();
@@ -1385,6 +1384,32 @@ __global__ __launch_bounds__(64) void k_decode4d(FieldDesc F, Params p, const ui
                         (int64_t)(4ull * ib[2] + z) * F.s[2] + (int64_t)(4ull * ib[3] + t) * F.s[3];
     for (uint32_t x = 0; x < nv[0]; x++) out[row + (int64_t)x * F.s[0]] = nonzero ? sc * (float)q[4 * lane + x] : 0.0f;
   }
+  __syncthreads();  // q is reused by the next block of a sequential walk
+  return used;
+}
+
+// decode: blocks at index[b] (variable, index stride 1) or b * maxbits (fixed), one wave per block
+__global__ __launch_bounds__(64) void k_decode4d(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                 const uint64_t* __restrict__ index, uint64_t base_bits)
+{
+  __shared__ int32_t q[256];
+  const uint32_t b = blockIdx.x;
+  BitReader r{in, base_bits + (index ? index[b] : (uint64_t)b * p.maxbits)};
+  decode4d_block(F, p, r, b, q, threadIdx.x);
+}
+
+// variable-rate stream without a block index (e.g. a zfpy stream): one wave walks the blocks in order, each block
+// starting where the previous one ended; the end bit goes to *end when asked
+__global__ __launch_bounds__(64) void k_decode4d_seq(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                     uint64_t base_bits, uint64_t* __restrict__ end)
+{
+  __shared__ int32_t q[256];
+  uint64_t pos = base_bits;
+  for (uint32_t b = 0; b < F.nblocks; b++) {
+    BitReader r{in, pos};
+    pos += decode4d_block(F, p, r, b, q, threadIdx.x);
+  }
+  if (end && threadIdx.x == 0) *end = pos;
 }
 
 // exclusive scan of per-block lengths: one "range" per block through k_scan_ranges (which also zeroes the words
@@ -2279,6 +2304,13 @@ hipError_t launch_decode4d(const FieldDesc& F, const Params& p, const uint64_t* 
                            uint64_t base_bits, void* stream)
 {
   k_decode4d<<<F.nblocks, 64, 0, S(stream)>>>(F, p, in, index, base_bits);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode4d_seq(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t base_bits,
+                               uint64_t* end, void* stream)
+{
+  k_decode4d_seq<<<1, 64, 0, S(stream)>>>(F, p, in, base_bits, end);
   return hipGetLastError();
 }
 

@@ -56,6 +56,8 @@ hipError_t launch_encode4d(const FieldDesc& F, const Params& p, uint32_t* lens, 
                            uint64_t* index, uint32_t index_shift, void* stream);
 hipError_t launch_decode4d(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
                            uint64_t base_bits, void* stream);
+hipError_t launch_decode4d_seq(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t base_bits,
+                               uint64_t* end, void* stream);
 hipError_t launch_scan_blocks(const uint32_t* lens, uint32_t nblocks, uint64_t* sums, uint64_t* base, uint64_t* total,
                               uint32_t* out32, void* stream);
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);

@@ -210,7 +210,7 @@ size_t gcow_encode_workspace_bytes(const zfp_input* field, const gcow_params* p)
 size_t gcow_index_entries(const zfp_input* field, uint32_t index_stride);
 
 /*
- * Encode field->data (DEVICE pointer, fp32 or bf16, 1-3 dims, any element strides) into d_out (device).
+ * Encode field->data (DEVICE pointer, fp32 or bf16, 1-4 dims, any element strides) into d_out (device).
  * The stream is byte-identical to sw/'s zfp_compress on the same values (headerless, LSB-first 64-bit words,
  * flushed with zero bits to a 64-bit boundary). *d_total_bits (device uint64, may be NULL) receives the unflushed
  * bit count. d_index (device, may be NULL) receives the bit offset of every index_stride-th block (1..256, power of

@@ -295,7 +295,7 @@ def read_header(words):
     w = np.zeros(3, np.uint64)
     src = np.ascontiguousarray(words, dtype=np.uint64)[:3]
     w[: len(src)] = src
-    dims, n, t, p = C.c_uint(), (C.c_size_t * 3)(), C.c_uint(), Params()
+    dims, n, t, p = C.c_uint(), (C.c_size_t * 4)(), C.c_uint(), Params()
     bits = lib().orc_read_header(_p(w, C.c_uint64), C.byref(dims), n, C.byref(t), C.byref(p))
     shape = tuple(reversed([n[i] for i in range(dims.value)])) if bits else ()
     return shape, t.value, p, int(bits)

@@ -723,9 +723,9 @@ uint64_t orc_decompress_at(float* data, unsigned dims, const size_t* n, const pt
 
 static uint64_t field_meta(unsigned dims, const size_t* n, unsigned zfp_type)
 {
-  /* sizes (48 bits: 48 / 24 / 16 per axis by dims), then dims - 1 (2 bits), then type - 1 (2 bits) */
+  /* sizes (48 bits: 48 / 24 / 16 / 12 per axis by dims), then dims - 1 (2 bits), then type - 1 (2 bits) */
   uint64_t meta = 0;
-  unsigned w = dims == 1 ? 48 : dims == 2 ? 24 : 16;
+  unsigned w = dims == 1 ? 48 : dims == 2 ? 24 : dims == 3 ? 16 : 12;
   for (int a = (int)dims - 1; a >= 0; a--) meta = (meta << w) + (uint64_t)(n[a] - 1);
   meta = (meta << 2) + (dims - 1);
   meta = (meta << 2) + (zfp_type - 1);
@@ -789,9 +789,8 @@ unsigned orc_read_header(const uint64_t* words, unsigned* dims, size_t* n, unsig
   meta >>= 2;
   *dims = (unsigned)(meta & 3u) + 1;
   meta >>= 2;
-  unsigned w = *dims == 1 ? 48 : *dims == 2 ? 24 : 16;
-  for (unsigned a = 0; a < 3; a++) n[a] = 0;
-  if (*dims > 3) return 0;
+  unsigned w = *dims == 1 ? 48 : *dims == 2 ? 24 : *dims == 3 ? 16 : 12;
+  for (unsigned a = 0; a < 4; a++) n[a] = 0;
   for (unsigned a = 0; a < *dims; a++) {
     n[a] = (size_t)(meta & ((1ull << w) - 1)) + 1;
     meta >>= w;

@@ -20,7 +20,9 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
-from gen_libzfp_fixtures import Z, ZFP_FLOAT, field, zstream  # noqa: E402
+import gen_libzfp_fixtures_4d  # noqa: E402,F401  (adds zfp_field_4d to gen_libzfp_fixtures.field)
+import gen_libzfp_fixtures as G  # noqa: E402
+from gen_libzfp_fixtures import Z, ZFP_FLOAT, zstream  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (input generator only)
 
 Z.zfp_write_header.restype = C.c_size_t
@@ -62,7 +64,7 @@ def with_header(arr, mode, compress=True):
     bs = Z.stream_open(buf.ctypes.data, buf.nbytes)
     Z.zfp_stream_set_bit_stream(zs, bs)
     Z.zfp_stream_rewind(zs)
-    fld = field(arr)
+    fld = G.field(arr)
     hbits = Z.zfp_write_header(zs, fld, HEADER_FULL)
     if compress:
         nbytes = Z.zfp_compress(zs, fld)
@@ -96,7 +98,7 @@ def with_header(arr, mode, compress=True):
 def main():
     cases, arrays = [], {}
     # header-only cases over every mode class and limit (no data needed: the header depends on shape + params)
-    shapes = [(1000,), (1,), (7, 100), (7, 6, 5), (1 << 20,)]
+    shapes = [(1000,), (1,), (7, 100), (7, 6, 5), (1 << 20,), (3, 4, 5, 6), (4096, 1, 2, 4096)]
     modes = [("rate", 16.0), ("rate", 8.0), ("rate", 2.5), ("rate", 128.0), ("rate", 129.0),
              ("acc", 1e-3), ("acc", 1e-6), ("acc", 0.5),
              ("prec", 1), ("prec", 20), ("prec", 64),
@@ -106,7 +108,7 @@ def main():
              ("expert", (5, 16657, 64, -10)), ("expert", (1, 16657, 128, -1074))]
     for shp in shapes:
         for mode in modes:
-            if mode[0] == "rate" and len(shp) == 1 and mode[1] > 100:
+            if mode[0] == "rate" and len(shp) in (1, 4) and mode[1] > 100:
                 continue
             arr = np.zeros(shp, np.float32)
             r = with_header(arr, mode, compress=False)
@@ -125,6 +127,7 @@ def main():
         "2d_10x9": O.gen_normal(90, 1.0, 7, False).reshape(10, 9),
         "2d_bump37": O.gen_bump2d(37),
         "3d_7x10x9": O.gen_normal(630, 1.0, 10, False).reshape(7, 10, 9),
+        "4d_3x6x5x7": O.gen_normal(630, 1.0, 11, False).reshape(3, 6, 5, 7),
     }
     smodes = [("rate", 16.0), ("rate", 8.0), ("acc", 1e-3), ("acc", 1e-6), ("prec", 20), ("expert", (10, 200, 30, -50))]
     for iname, arr in inputs.items():

@@ -666,3 +666,13 @@ def test_4d_random_and_bf16(gc, orc):
         _check_vs_oracle(gc, orc, a, op, index_stride=0 if op.minbits == op.maxbits else 1)
     bf = (a.view(np.uint32) >> 16).astype(np.uint16)
     _check_vs_oracle(gc, orc, bf, orc.accuracy(1e-3), index_stride=1, decode=False)
+
+
+@pytest.mark.parametrize("stride", [0, 4])
+def test_4d_variable_rate_sequential_decode(gc, orc, stride):
+    """4-D variable-rate streams without a stride-1 block index decode by one wave walking the blocks in order."""
+    rng = np.random.default_rng(45 + stride)
+    a = (rng.standard_normal((5, 9, 4, 6)) * 1e-1).astype(np.float32)
+    a[1:3] = 0.0  # zero blocks: one bit each
+    for op in (orc.accuracy(1e-5), orc.precision(14), orc.expert(30, 600, 24, -20)):
+        _check_vs_oracle(gc, orc, a, op, index_stride=stride)
