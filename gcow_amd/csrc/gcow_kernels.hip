@@ -916,17 +916,61 @@ __device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uin
   return len;
 }
 
-// Variable-rate 1-D pass 1: per-range sums of block bit lengths (closed-form coder; generic for special blocks).
+// Bit length of a variable-rate 1-D block (same domain as encode_block1d_var; Inf/NaN -> special) from the leading
+// one-bit planes L_i of its four negabinary coefficients alone. With n_k = 1 + max{i : L_i >= k} the prefix after
+// plane k (encode.c:279-339 carries n across planes), plane k costs n_{k+1} verbatim bits plus, when n_{k+1} < 4,
+// either one '0' (nothing new) or m + (q == 3 ? 3 : q + 2) - n_{k+1} bits (m new one-bits, the last at q: one group
+// flag each, the run up to q, a closing '0' unless q is the implied last position). With R_j = max_{i >= j} L_i summed
+// over planes kmin .. 31:
+//   sum_j max(0, R_j - kmin) + (32 - max(kmin, L_3)) + #{j : L_j = R_j >= kmin}
+//   + sum_j [R_j >= kmin, last index at its level] (j < 3 ? j + 1 : 2) - sum_j [R_j >= kmin, first at its level] j.
+__device__ __forceinline__ uint32_t count_block1d_var(const float* f, int minexp, uint32_t maxprec, bool& special)
+{
+  const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
+  const uint32_t a2 = __float_as_uint(f[2]) & 0x7fffffffu, a3 = __float_as_uint(f[3]) & 0x7fffffffu;
+  const uint32_t m = max(max(a0, a1), max(a2, a3));
+  special = m >= 0x7f800000u;
+  const uint32_t E = special ? 150u : (m >> 23);
+  const int emax = (int)max(E, 1u) - 126;
+  const int prec = min((int)maxprec, max(0, emax - minexp + 4));
+  if (m == 0 || prec == 0) return 1u;
+  const int kmin = prec < 32 ? 32 - prec : 0;
+  const bool tiny = E < 29u;
+  const float s = __uint_as_float((283u - (tiny ? 150u : E)) << 23);
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = tiny ? (int32_t)0x80000000 : (int32_t)(f[i] * s);
+  fwd_lift(q[0], q[1], q[2], q[3]);
+  int Lv[4], R[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t u = ((uint32_t)q[i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+    Lv[i] = u ? 31 - (int)__builtin_clz(u) : -1;
+  }
+  R[3] = Lv[3];
+  R[2] = max(Lv[2], R[3]);
+  R[1] = max(Lv[1], R[2]);
+  R[0] = max(Lv[0], R[1]);
+  int len = 9 + 32 - max(kmin, Lv[3]);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const bool on = R[j] >= kmin;
+    len += max(0, R[j] - kmin);
+    len += (on && Lv[j] == R[j]) ? 1 : 0;
+    if (j < 3) len += (on && R[j + 1] < R[j]) ? j + 1 : 0;
+    else len += on ? 2 : 0;
+    if (j > 0) len -= (on && R[j - 1] > R[j]) ? j : 0;
+  }
+  return (uint32_t)len;
+}
+
+// Variable-rate 1-D pass 1: per-range sums of block bit lengths (closed form from the leading planes; generic for
+// Inf/NaN blocks).
 // Each lane codes U consecutive blocks per step (tile = 256 U blocks).
 template <int DT, int U>
 __global__ __launch_bounds__(256) void k_count1d_var(FieldDesc F, Params p, uint32_t range, uint64_t* __restrict__ sums)
 {
-  __shared__ uint16_t tab[80];
-  __shared__ uint32_t tab2[1280];
   __shared__ uint64_t red[4];
-  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab5.v[t];
-  if (threadIdx.x < 80) tab[threadIdx.x] = plane_entry4(threadIdx.x);
-  __syncthreads();
   const uint64_t b0 = (uint64_t)blockIdx.x * range;
   const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
   uint64_t acc = 0;
@@ -942,7 +986,7 @@ __global__ __launch_bounds__(256) void k_count1d_var(FieldDesc F, Params p, uint
     for (int k = 0; k < U; k++) {
       const uint64_t b = t0 + (uint64_t)threadIdx.x * U + k;
       bool special;
-      uint32_t len = encode_block1d_var<false>(f[k], tab, tab2, p.minexp, p.maxprec, nullptr, special);
+      uint32_t len = count_block1d_var(f[k], p.minexp, p.maxprec, special);
       if (special && b < b1) {
         CountWriter w;
         len = encode_block<1>(w, f[k], p);
