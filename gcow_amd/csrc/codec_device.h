@@ -434,6 +434,63 @@ __device__ __forceinline__ uint32_t encode_block(W& w, const float* f, const Par
   return 9 + bits;
 }
 
+// Bit length of encode_ints' untruncated output from the coefficients' leading one-bit planes alone (B = 4^d). With
+// L_j the leading plane of u_j (-1 for 0) and R_j = max_{i >= j} L_i, the prefix after plane k is
+// n_k = #{j : R_j >= k}; plane k costs n_{k+1} verbatim bits plus, while n_{k+1} < B, one '0' if no coefficient turns
+// significant, else m + (q == B-1 ? B-1 : q+2) - n_{k+1} (m new one-bits, the last at q; encode.c:279-339). Summed over
+// planes kmin .. 31:
+//   sum_j max(0, R_j - kmin) + 32 - max(kmin, L_{B-1}) + #{j : L_j = R_j >= kmin}
+//   + sum_{j last at its level, R_j >= kmin} (j < B-1 ? j+1 : B-2) - sum_{j first at its level, R_j >= kmin} j.
+template <int B>
+__device__ __forceinline__ uint32_t encode_ints_length(const uint32_t* u, uint32_t maxprec)
+{
+  const int kmin = maxprec < 32 ? 32 - (int)maxprec : 0;
+  const int Llast = u[B - 1] ? 31 - (int)__builtin_clz(u[B - 1]) : -1;
+  int len = 32 - max(kmin, Llast);
+  int Rn = Llast;  // R_{j+1}
+  len += max(0, Llast - kmin) + (Llast >= kmin ? 1 + (B - 2) : 0);
+#pragma unroll
+  for (int j = B - 2; j >= 0; j--) {
+    const int Lj = u[j] ? 31 - (int)__builtin_clz(u[j]) : -1;
+    const int Rj = max(Lj, Rn);
+    const bool on = Rj >= kmin, step = Rj > Rn;
+    len += max(0, Rj - kmin);
+    len += (on && Lj == Rj) ? 1 : 0;
+    len += (on && step) ? j + 1 : 0;               // j is the last index at level R_j
+    len -= (Rn >= kmin && step) ? j + 1 : 0;       // j + 1 is the first index at level R_{j+1}
+    Rn = Rj;
+  }
+  return (uint32_t)len;
+}
+
+// encode_block's return value without coding: same header / cast / transform / reorder, then the closed-form length
+// clipped to the budget and padded to minbits.
+template <int D>
+__device__ __forceinline__ uint32_t count_block(const float* f, const Params& p)
+{
+  constexpr int B = Dim<D>::B;
+  float fa[B];
+#pragma unroll
+  for (int i = 0; i < B; i++) fa[i] = f[i];
+  const int emax = block_emax<B>(fa);
+  const uint32_t prec = precision(emax, p.maxprec, p.minexp, D);
+  const uint32_t be = prec ? (uint32_t)(emax + 127) : 0u;
+  if (!be) return p.minbits > 1u ? p.minbits : 1u;
+  int32_t q[B];
+  const float s = cast_scale(emax);
+#pragma unroll
+  for (int i = 0; i < B; i++) q[i] = cast1(fa[i], s);
+  fwd_xform<D>(q);
+  uint32_t u[B];
+  fwd_reorder<D>(u, q);
+  const uint32_t maxb = p.maxbits - 9u;
+  const uint32_t minb = p.minbits - (p.minbits < 9u ? p.minbits : 9u);
+  const uint32_t budget = exceeded_maxbits(maxb, prec, B) ? maxb : 0xffffffffu;
+  uint32_t bits = encode_ints_length<B>(u, prec);
+  bits = bits < budget ? bits : budget;
+  return 9 + (bits < minb ? minb : bits);
+}
+
 // ------------------------------------------------------------------------------------------------ reader / decoder
 struct BitReader {
   const uint64_t* w;

@@ -705,8 +705,7 @@ __global__ __launch_bounds__(T) void k_count(FieldDesc F, Params p, uint32_t ran
   for (uint64_t b = b0 + threadIdx.x; b < b1; b += T) {
     float f[B];
     gather_block<D, DT>(F, (uint32_t)b, f);
-    CountWriter w;
-    acc += encode_block<D>(w, f, p);
+    acc += count_block<D>(f, p);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
@@ -782,8 +781,7 @@ __global__ __launch_bounds__(T) void k_encode_tiles(FieldDesc F, Params p, uint3
       if (FIXED) {
         len = p.maxbits;
       } else {
-        CountWriter cw;
-        len = encode_block<D>(cw, f, p);
+        len = count_block<D>(f, p);
       }
     }
     uint32_t tile_total;
@@ -988,8 +986,7 @@ __global__ __launch_bounds__(256) void k_count1d_var(FieldDesc F, Params p, uint
       bool special;
       uint32_t len = count_block1d_var(f[k], p.minexp, p.maxprec, special);
       if (special && b < b1) {
-        CountWriter w;
-        len = encode_block<1>(w, f[k], p);
+        len = count_block<1>(f[k], p);
       }
       acc += b < b1 ? len : 0u;
     }
@@ -1044,8 +1041,7 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
       len[k] = encode_block1d_var<true>(f[k], tab, tab2, p.minexp, p.maxprec, c[k], sp[k]);
       sp[k] = sp[k] && valid;
       if (sp[k]) {
-        CountWriter cw;
-        len[k] = encode_block<1>(cw, f[k], p);
+        len[k] = count_block<1>(f[k], p);
       }
       len[k] = valid ? len[k] : 0u;
       lsum += len[k];
