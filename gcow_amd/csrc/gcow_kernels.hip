@@ -964,38 +964,88 @@ __device__ __forceinline__ uint32_t count_block1d_var(const float* f, int minexp
 
 // Variable-rate 1-D pass 1: per-range sums of block bit lengths (closed form from the leading planes; generic for
 // Inf/NaN blocks).
-// Each lane codes U consecutive blocks per step (tile = 256 U blocks).
+// Tiles of 256 U blocks; contiguous bf16 input takes coalesced 16-B loads with the next tile prefetched.
 template <int DT, int U>
 __global__ __launch_bounds__(256) void k_count1d_var(FieldDesc F, Params p, uint32_t range, uint64_t* __restrict__ sums)
 {
+  constexpr uint32_t TILE = 256u * U;
+  constexpr int BPL = DT == DT_BF16 ? 2 : 1;  // blocks per 16-B load
+  constexpr int NL = U / BPL;                 // 16-B loads per lane per tile
+  static_assert(U % BPL == 0, "U must hold whole 16-B loads");
   __shared__ uint64_t red[4];
+  const uint32_t tid = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * range;
   const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
   uint64_t acc = 0;
-  for (uint64_t t0 = b0; t0 < b1; t0 += 256 * U) {  // wave-uniform trip count (the coder uses wave votes)
+  uint64_t t0 = b0;
+  // Contiguous, 16-B aligned bf16 input: whole tiles of full blocks read with coalesced 16-B loads (load j of lane t
+  // covers blocks t0 + (256 j + t) BPL ..; the sum is order-free), the next tile's loads issued before this tile is
+  // counted (C5 acc 1e-6 0.878 -> 0.843 ms). The same form measured slower for fp32 (0.876 -> 1.043 ms): fp32 keeps the
+  // per-lane gather below.
+  if (DT == DT_BF16 && F.vec && F.s[0] == 1 && (((uintptr_t)F.data) & 15u) == 0) {
+    const uint64_t lim = min<uint64_t>(b1, F.n[0] / 4);
+    const uint64_t tend = lim > b0 ? b0 + (lim - b0) / TILE * TILE : b0;
+    const uint4* src = (const uint4*)F.data;  // 16-B units: one f32 block or two bf16 blocks
+    uint4 cur[NL], nxt[NL];
+    if (t0 < tend) {
+#pragma unroll
+      for (int j = 0; j < NL; j++) cur[j] = src[t0 / BPL + 256u * j + tid];
+    }
+    for (; t0 < tend; t0 += TILE) {
+      if (t0 + TILE < tend) {
+#pragma unroll
+        for (int j = 0; j < NL; j++) nxt[j] = src[(t0 + TILE) / BPL + 256u * j + tid];
+      }
+#pragma unroll
+      for (int j = 0; j < NL; j++) {
+        float f[BPL][4];
+        if constexpr (DT == DT_BF16) {
+          const uint32_t w[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            f[h][0] = __uint_as_float(w[2 * h] << 16);
+            f[h][1] = __uint_as_float(w[2 * h] & 0xffff0000u);
+            f[h][2] = __uint_as_float(w[2 * h + 1] << 16);
+            f[h][3] = __uint_as_float(w[2 * h + 1] & 0xffff0000u);
+          }
+        } else {
+          f[0][0] = __uint_as_float(cur[j].x); f[0][1] = __uint_as_float(cur[j].y);
+          f[0][2] = __uint_as_float(cur[j].z); f[0][3] = __uint_as_float(cur[j].w);
+        }
+#pragma unroll
+        for (int h = 0; h < BPL; h++) {
+          bool special;
+          uint32_t len = count_block1d_var(f[h], p.minexp, p.maxprec, special);
+          if (special) len = count_block<1>(f[h], p);
+          acc += len;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NL; j++) cur[j] = nxt[j];
+    }
+  }
+  for (; t0 < b1; t0 += TILE) {  // the rest (partial tiles, the padded last block, strided input)
     float f[U][4];
 #pragma unroll
     for (int k = 0; k < U; k++) {
-      const uint64_t b = t0 + (uint64_t)threadIdx.x * U + k;
+      const uint64_t b = t0 + (uint64_t)tid * U + k;
       f[k][0] = f[k][1] = f[k][2] = f[k][3] = 0.0f;
       if (b < b1) gather_block<1, DT>(F, (uint32_t)b, f[k]);
     }
 #pragma unroll
     for (int k = 0; k < U; k++) {
-      const uint64_t b = t0 + (uint64_t)threadIdx.x * U + k;
+      const uint64_t b = t0 + (uint64_t)tid * U + k;
       bool special;
       uint32_t len = count_block1d_var(f[k], p.minexp, p.maxprec, special);
-      if (special && b < b1) {
-        len = count_block<1>(f[k], p);
-      }
+      if (special && b < b1) len = count_block<1>(f[k], p);
       acc += b < b1 ? len : 0u;
     }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  if ((tid & 63) == 0) red[tid >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) sums[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (tid == 0) sums[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 // Variable-rate 1-D pass 2: k_encode_tiles with the closed-form coder over tiles of 256 U blocks (U consecutive
