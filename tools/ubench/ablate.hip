@@ -784,6 +784,10 @@ extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, i
     case 62: gcow::k_chunk5<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 63: gcow::k_chunk5<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 9: gcow::k_floor1<false><<<(nfull + 255) / 256, 256, 0, st>>>((const float4*)in, nfull, (uint2*)out); break;
+    // one-shot, two blocks per lane (16-B store): the access shape a paired-store encoder would have
+    case 64: gcow::k_floor2<false><<<(nfull / 2 + 255) / 256, 256, 0, st>>>((const float4*)in, nfull / 2, (uint4*)out); break;
+    case 65: gcow::k_floor2<true><<<(nfull / 2 + 255) / 256, 256, 0, st>>>((const float4*)in, nfull / 2, (uint4*)out); break;
+    case 66: gcow::k_floor1<true><<<(nfull + 255) / 256, 256, 0, st>>>((const float4*)in, nfull, (uint2*)out); break;
   }
   return (int)hipGetLastError();
 }
