@@ -2275,6 +2275,7 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
   else k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   k_scan_ranges<<<1, 1024, 0, st>>>(ws_sums, plan.nranges, ws_base, d_total, out32, d_base);
   if (var1d) {
+    // U = 4 blocks per lane (U = 8 measured 0.835 -> 1.083 ms on C5 acc 1e-6: register pressure)
     k_encode1d_var<DT, 4><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_base, out32, index, index_shift);
     return hipGetLastError();
   }
