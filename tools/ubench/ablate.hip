@@ -705,7 +705,53 @@ __global__ __launch_bounds__(256) void k_cfloor(const void* __restrict__ in, uin
     }
   }
 }
+
+// 3-D fixed-rate split (C3, rate 8): STAGE 0 = gather + emax + cast + lift + reorder, folded into the block's words;
+// STAGE 1 = + the two 32 x 32 bit transposes; (the full kernel is k_encode3d_fixed)
+template <int STAGE>
+__global__ __launch_bounds__(256) void k_c3_split(FieldDesc F, Params p, uint32_t* __restrict__ out32)
+{
+  constexpr uint32_t WPB = 16;
+  extern __shared__ uint32_t lds_w[];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * 256u;
+  const uint32_t nvalid = min(256u, F.nblocks - b0);
+  uint32_t* mine = lds_w + tid * (WPB + 1);
+  if (tid < nvalid) {
+    float f[64];
+    gather_block<3, DT_F32>(F, b0 + tid, f);
+    const int emax = block_emax<64>(f);
+    int32_t q[64];
+    const float sc = cast_scale(emax);
+#pragma unroll
+    for (int i = 0; i < 64; i++) q[i] = cast1(f[i], sc);
+    fwd_xform<3>(q);
+    uint32_t u[64];
+    fwd_reorder<3>(u, q);
+    if (STAGE >= 1) {
+      transpose32(u);
+      transpose32(u + 32);
+    }
+#pragma unroll
+    for (int w = 0; w < 16; w++) mine[w] = u[w] ^ u[w + 16] ^ u[w + 32] ^ u[w + 48];
+  }
+  __syncthreads();
+  uint32_t* dst = out32 + (uint64_t)b0 * WPB;
+  for (uint32_t j = tid; j < nvalid * WPB; j += 256) dst[j] = lds_w[(j / WPB) * (WPB + 1) + (j % WPB)];
+}
 }  // namespace gcow
+
+static gcow::FieldDesc c3_field(const void* in)
+{
+  gcow::FieldDesc F{};
+  F.data = in;
+  F.n[0] = F.n[1] = F.n[2] = 512; F.n[3] = 1;
+  F.s[0] = 1; F.s[1] = 512; F.s[2] = 512 * 512; F.s[3] = 0;
+  F.bx = F.by = F.bz = 128; F.bw = 1;
+  F.nblocks = 128u * 128u * 128u;
+  F.dims = 3; F.dtype = gcow::DT_F32; F.vec = 1;
+  return F;
+}
 
 extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, int wgs, void* stream)
 {
@@ -787,6 +833,15 @@ extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, i
     // one-shot, two blocks per lane (16-B store): the access shape a paired-store encoder would have
     case 64: gcow::k_floor2<false><<<(nfull / 2 + 255) / 256, 256, 0, st>>>((const float4*)in, nfull / 2, (uint4*)out); break;
     case 65: gcow::k_floor2<true><<<(nfull / 2 + 255) / 256, 256, 0, st>>>((const float4*)in, nfull / 2, (uint4*)out); break;
+    case 70: case 71: case 72: {
+      const gcow::FieldDesc F = c3_field(in);
+      const gcow::Params p{512, 512, 64, -1074};
+      const size_t lds = 256 * 17 * 4;
+      if (mode == 70) gcow::k_encode3d_fixed<gcow::DT_F32, 16><<<F.nblocks / 256, 256, lds, st>>>(F, p, (uint32_t*)out);
+      else if (mode == 71) gcow::k_c3_split<0><<<F.nblocks / 256, 256, lds, st>>>(F, p, (uint32_t*)out);
+      else gcow::k_c3_split<1><<<F.nblocks / 256, 256, lds, st>>>(F, p, (uint32_t*)out);
+      break;
+    }
     case 66: gcow::k_floor1<true><<<(nfull + 255) / 256, 256, 0, st>>>((const float4*)in, nfull, (uint2*)out); break;
   }
   return (int)hipGetLastError();
