@@ -1072,14 +1072,48 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
   const uint64_t first_word = base >> 5;
   const bool first_shared = (base & 31) != 0;
   uint32_t carry = 0;
+  // Contiguous, 16-B aligned bf16: a lane's U consecutive blocks are U/2 16-B loads, issued one tile ahead (before
+  // this tile's scan / LDS / store rounds) for every tile made of full blocks only.
+  constexpr bool WIDE = DT == DT_BF16 && U % 2 == 0;
+  constexpr int NW = WIDE ? U / 2 : 1;
+  const bool wide = WIDE && F.vec && F.s[0] == 1 && (((uintptr_t)F.data) & 15u) == 0;
+  const uint64_t full_end = min<uint64_t>(b1, F.n[0] / 4);  // blocks below this are full
+  const uint4* src = (const uint4*)F.data;
+  uint4 nxt[NW];
+  auto wide_tile = [&](uint64_t t) { return wide && t + T * U <= full_end; };
+  if (wide_tile(b0)) {
+#pragma unroll
+    for (int h = 0; h < NW; h++) nxt[h] = src[(b0 + (uint64_t)tid * U) / 2 + h];
+  }
   __syncthreads();
   for (uint64_t t0 = b0; t0 < b1; t0 += T * U) {
     float f[U][4];
+    if (wide_tile(t0)) {
+      uint4 cur[NW];
 #pragma unroll
-    for (int k = 0; k < U; k++) {
-      const uint64_t b = t0 + (uint64_t)tid * U + k;
-      f[k][0] = f[k][1] = f[k][2] = f[k][3] = 0.0f;
-      if (b < b1) gather_block<1, DT>(F, (uint32_t)b, f[k]);
+      for (int h = 0; h < NW; h++) cur[h] = nxt[h];
+      if (wide_tile(t0 + T * U)) {
+#pragma unroll
+        for (int h = 0; h < NW; h++) nxt[h] = src[(t0 + T * U + (uint64_t)tid * U) / 2 + h];
+      }
+#pragma unroll
+      for (int h = 0; h < NW; h++) {
+        const uint32_t w[4] = {cur[h].x, cur[h].y, cur[h].z, cur[h].w};
+#pragma unroll
+        for (int g = 0; g < 2 && 2 * h + g < U; g++) {
+          f[2 * h + g][0] = __uint_as_float(w[2 * g] << 16);
+          f[2 * h + g][1] = __uint_as_float(w[2 * g] & 0xffff0000u);
+          f[2 * h + g][2] = __uint_as_float(w[2 * g + 1] << 16);
+          f[2 * h + g][3] = __uint_as_float(w[2 * g + 1] & 0xffff0000u);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; k++) {
+        const uint64_t b = t0 + (uint64_t)tid * U + k;
+        f[k][0] = f[k][1] = f[k][2] = f[k][3] = 0.0f;
+        if (b < b1) gather_block<1, DT>(F, (uint32_t)b, f[k]);
+      }
     }
     uint64_t c[U][3];
     uint32_t len[U];
