@@ -1073,7 +1073,8 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
   const bool first_shared = (base & 31) != 0;
   uint32_t carry = 0;
   // Contiguous, 16-B aligned bf16: a lane's U consecutive blocks are U/2 16-B loads, issued one tile ahead (before
-  // this tile's scan / LDS / store rounds) for every tile made of full blocks only.
+  // this tile's scan / LDS / store rounds) for every tile made of full blocks only. (The same for fp32, U 16-B loads
+  // per lane, measured slower: 0.875 -> 0.968 ms at accuracy 1e-6.)
   constexpr bool WIDE = DT == DT_BF16 && U % 2 == 0;
   constexpr int NW = WIDE ? U / 2 : 1;
   const bool wide = WIDE && F.vec && F.s[0] == 1 && (((uintptr_t)F.data) & 15u) == 0;
