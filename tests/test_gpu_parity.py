@@ -541,12 +541,38 @@ def test_c5_full_size_bf16_accuracy(gc, orc):
     assert np.array_equal(e.stream().cpu().numpy().view(np.uint64), w_ref)
 
 
+@pytest.mark.parametrize("nblocks", [1, 1023, 1024, 1025, 2048 + 5, 70001])
+@pytest.mark.parametrize("layout", ["contig", "offset1", "offset8", "stride2"])
+def test_var1d_bf16_load_paths(gc, orc, nblocks, layout):
+    """Variable-rate 1-D bf16: the coalesced 16-B load paths of the count and encode passes (contiguous, 16-B aligned,
+    whole tiles of 1024 full blocks) and the per-lane gather they fall back to (a 2-B or 16-B offset view, a strided
+    view, partial tiles, a padded last block) give the oracle's stream and block index."""
+    n = 4 * nblocks - (1 if nblocks > 1 else 0)
+    a = orc.gen_normal(n, 1e-3, 500 + nblocks, True)
+    hb = (a.view(np.uint32) >> 16).astype(np.uint16)
+    op = orc.accuracy(1e-6)
+    w_ref, bits_ref = orc.compress(hb, op)
+    pad = {"contig": 0, "offset1": 1, "offset8": 8, "stride2": 0}[layout]
+    step = 2 if layout == "stride2" else 1
+    big = np.zeros(pad + step * n, np.uint16)
+    big[pad::step] = hb
+    x = torch.from_numpy(big).cuda().view(torch.bfloat16)[pad::step]
+    assert x.numel() == n
+    e = gc.encode(x, P(gc, op), index_stride=16)
+    torch.cuda.synchronize()
+    assert e.bits == bits_ref
+    assert e.to_bytes() == w_ref.tobytes()
+    d = gc.decode(e)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy().view(np.uint32), orc.decompress(w_ref, hb.shape, op).view(np.uint32))
+
+
 @pytest.mark.parametrize("nblocks", [1, 511, 512, 513, 1024, 5000, 100003])
 @pytest.mark.parametrize("mode", ["acc1e-3", "sparse"])
-def test_var1d_single_pass_tiles(gc, orc, nblocks, mode):
-    """Single-pass variable-rate 1-D encoder (512-block tiles, decoupled look-back) across tile boundaries: partial
-    last tile and block, exact multiples, mostly-zero tiles (1-bit blocks: tile boundaries on 32-bit words), stream +
-    block index + decode vs the oracle."""
+def test_var1d_tiles(gc, orc, nblocks, mode):
+    """Variable-rate 1-D encoder (count pass, range scan, tiles of 1024 blocks) across tile boundaries: partial last
+    tile and block, exact multiples, mostly-zero tiles (1-bit blocks: tile boundaries on 32-bit words), stream + block
+    index + decode vs the oracle."""
     n = 4 * nblocks - (1 if nblocks > 1 else 0)
     if mode == "acc1e-3":
         a = orc.gen_normal(n, 1e-3, 1000 + nblocks, True)
