@@ -446,21 +446,23 @@ __device__ __forceinline__ uint32_t encode_ints_length(const uint32_t* u, uint32
 {
   const int kmin = maxprec < 32 ? 32 - (int)maxprec : 0;
   const int Llast = u[B - 1] ? 31 - (int)__builtin_clz(u[B - 1]) : -1;
-  int len = 32 - max(kmin, Llast);
+  // sum_j max(0, R_j - kmin) = sum_j max(R_j, kmin) - B kmin. The last-/first-at-level sums cancel wherever both
+  // neighbours are >= kmin (R is non-increasing), leaving j + 1 at the one j with R_j >= kmin > R_{j+1}: with
+  // c = #{j : R_j >= kmin} they add c, or B - 2 when c = B.
+  int len = 32 - max(kmin, Llast) - B * kmin + max(Llast, kmin) + (Llast >= kmin ? 1 : 0);
+  int c = Llast >= kmin ? 1 : 0;
   int Rn = Llast;  // R_{j+1}
-  len += max(0, Llast - kmin) + (Llast >= kmin ? 1 + (B - 2) : 0);
 #pragma unroll
   for (int j = B - 2; j >= 0; j--) {
     const int Lj = u[j] ? 31 - (int)__builtin_clz(u[j]) : -1;
     const int Rj = max(Lj, Rn);
-    const bool on = Rj >= kmin, step = Rj > Rn;
-    len += max(0, Rj - kmin);
+    const bool on = Rj >= kmin;
+    len += max(Rj, kmin);
     len += (on && Lj == Rj) ? 1 : 0;
-    len += (on && step) ? j + 1 : 0;               // j is the last index at level R_j
-    len -= (Rn >= kmin && step) ? j + 1 : 0;       // j + 1 is the first index at level R_{j+1}
+    c += on ? 1 : 0;
     Rn = Rj;
   }
-  return (uint32_t)len;
+  return (uint32_t)(len + (c == B ? B - 2 : c));
 }
 
 // encode_block's return value without coding: same header / cast / transform / reorder, then the closed-form length

@@ -921,7 +921,8 @@ __device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uin
 // flag each, the run up to q, a closing '0' unless q is the implied last position). With R_j = max_{i >= j} L_i summed
 // over planes kmin .. 31:
 //   sum_j max(0, R_j - kmin) + (32 - max(kmin, L_3)) + #{j : L_j = R_j >= kmin}
-//   + sum_j [R_j >= kmin, last index at its level] (j < 3 ? j + 1 : 2) - sum_j [R_j >= kmin, first at its level] j.
+//   + sum_j [R_j >= kmin, last index at its level] (j < 3 ? j + 1 : 2) - sum_j [R_j >= kmin, first at its level] j,
+// where the last two sums cancel except where R crosses kmin (see encode_ints_length).
 __device__ __forceinline__ uint32_t count_block1d_var(const float* f, int minexp, uint32_t maxprec, bool& special)
 {
   const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
@@ -949,17 +950,17 @@ __device__ __forceinline__ uint32_t count_block1d_var(const float* f, int minexp
   R[2] = max(Lv[2], R[3]);
   R[1] = max(Lv[1], R[2]);
   R[0] = max(Lv[0], R[1]);
-  int len = 9 + 32 - max(kmin, Lv[3]);
+  // the last-/first-at-level terms cancel except across kmin: with c = #{j : R_j >= kmin} they sum to c (c < 4) or 2
+  int len = 9 + 32 - max(kmin, Lv[3]) - 4 * kmin;
+  int c = 0;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const bool on = R[j] >= kmin;
-    len += max(0, R[j] - kmin);
+    len += max(R[j], kmin);
     len += (on && Lv[j] == R[j]) ? 1 : 0;
-    if (j < 3) len += (on && R[j + 1] < R[j]) ? j + 1 : 0;
-    else len += on ? 2 : 0;
-    if (j > 0) len -= (on && R[j - 1] > R[j]) ? j : 0;
+    c += on ? 1 : 0;
   }
-  return (uint32_t)len;
+  return (uint32_t)(len + (c == 4 ? 2 : c));
 }
 
 // Variable-rate 1-D pass 1: per-range sums of block bit lengths (closed form from the leading planes; generic for

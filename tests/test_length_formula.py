@@ -15,18 +15,38 @@ def length_formula(u, prec):
     B = len(u)
     kmin = 32 - prec if prec < 32 else 0
     last = _lead(u[B - 1])
-    n = 32 - max(kmin, last) + max(0, last - kmin) + ((1 + B - 2) if last >= kmin else 0)
+    n = 32 - max(kmin, last) - B * kmin + max(last, kmin) + (1 if last >= kmin else 0)
+    c = 1 if last >= kmin else 0
     rn = last
     for j in range(B - 2, -1, -1):
         lj = _lead(u[j])
         rj = max(lj, rn)
-        on, step = rj >= kmin, rj > rn
-        n += max(0, rj - kmin)
+        on = rj >= kmin
+        n += max(rj, kmin)
         n += 1 if (on and lj == rj) else 0
-        n += j + 1 if (on and step) else 0
-        n -= j + 1 if (rn >= kmin and step) else 0
+        c += 1 if on else 0
         rn = rj
-    return n
+    return n + (B - 2 if c == B else c)
+
+
+def length_per_plane(u, prec):
+    """The unsimplified sum over planes: n_{k+1} verbatim bits plus the group part of plane k."""
+    B = len(u)
+    kmin = 32 - prec if prec < 32 else 0
+    lead = [_lead(v) for v in u]
+    total, n = 0, 0
+    for k in range(31, kmin - 1, -1):
+        nk = max([j + 1 for j in range(B) if lead[j] >= k], default=0)
+        total += n
+        if n < B:
+            if nk == n:
+                total += 1
+            else:
+                m = sum(1 for j in range(n, B) if lead[j] == k)
+                q = nk - 1
+                total += m + (B - 1 if q == B - 1 else q + 2) - n
+        n = nk
+    return total
 
 
 def _blocks(rng, size, count):
@@ -49,6 +69,7 @@ def test_length_formula_matches_coder(orc, size):
         words[:] = 0
         _, _, bits = orc.encode_ints(u, 1 << 30, prec, words=words)
         assert length_formula(u, prec) == bits, (u.tolist(), prec)
+        assert length_per_plane(u, prec) == bits, (u.tolist(), prec)
 
 
 def test_length_formula_extremes(orc):
