@@ -1,20 +1,37 @@
 #!/usr/bin/env python3
-"""bench.py -- device-resident fp32 -> ZFP encode throughput (BASELINE.json metric), 1..N MI355X.
+"""bench.py -- device-resident fp32 -> ZFP encode throughput (BASELINE.json metric) on 1..N MI355X.
 
 Workload (BASELINE configs[1] = C2): a 256 Mi-float contiguous fp32 gradient bucket per GPU (1-D, 4-value blocks),
-fixed rate 16 (the caller's default, hw/models/train_imagenet.py:155), inputs resident in HBM before timing.
-A step = one encode of the whole bucket (one gfx950 kernel launch). N > 1: one process per GPU, each encodes its
-own 256 Mi shard of an N x 1 GiB bucket (weak scaling, the C4 sharding); the RCCL all-gather of the compressed
-shards is timed separately and reported under "allgather" (it is the exchange step, not the encode metric).
+fixed rate 16 (the caller's default, hw/models/train_imagenet.py:155), inputs resident in HBM before timing. A step is
+one encode of the whole bucket (one gfx950 kernel launch). `value` = all ranks' input bytes / the max-over-ranks time
+of exactly --steps steps after --warmup untimed ones (weak scaling: every rank encodes its own 256 Mi shard of an
+N x 1 GiB bucket, the C4 sharding; no collective on the encode path).
 
+`python bench.py --gpus N` with N > 1 and no torchrun environment launches N worker processes itself (torchrun on
+127.0.0.1, before this process touches the GPU); under torchrun (the driver's launch) it is one of the ranks.
+
+Extra objects on the same JSON line (they never change `value`):
+  roofline          the encode kernel's HIP-event time vs the HBM roofline (read-only bytes per BASELINE.md, and
+                    read + write), traffic = rocprofv3 PMC bytes per launch from profiles/ (traffic_source names it)
+  per_launch_ms     first / median / max kernel time over the timed steps (the clock ramps under a burst of launches)
+  steady_state      the same kernel after >= 0.25 s of back-to-back launches
+  N > 1:  encode_allgather (C4 exchange: encode + RCCL all-gather of the compressed shards, gathered stream checked
+          against the oracle on sampled ranges of every shard), subgroups (1/2/4/.. ranks over dist.new_group),
+          strong (8 GiB split k ways), c5_sharded (bf16 accuracy 1e-6: encode + length exchange + padded all-gather
+          + one-launch stitch, checked against the oracle at every shard start)
+  N = 1:  host_e2e (pinned H2D + encode + D2H; PCIe-inclusive), configs (C3 512^3 rate 8 / accuracy 1e-3 encode +
+          decode, C5 bf16 accuracy 1e-6 / 1e-3 device and host path), cpu_baseline (rank 0)
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import platform
+import socket
+import statistics
 import subprocess
 import sys
 import time
@@ -25,67 +42,126 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from gcow_amd import codec  # noqa: E402
-
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table); 6.29 TB/s measured float4 copy
 N_VALUES = 256 * 1024 * 1024
+SEED = 0x67636F77
+METRIC = "GiB/s device-resident fp32->ZFP encode, 256Mi-float bucket, 1/2/4/8 GPU"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rate", type=float, default=16.0)
     ap.add_argument("--values", type=int, default=N_VALUES)
+    ap.add_argument("--strong-gib", type=float, default=8.0, help="C4 strong-scaling bucket (GiB of fp32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-allgather", action="store_true")
-    ap.add_argument("--no-host-e2e", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--no-extras", action="store_true", help="only the headline measurement")
+    ap.add_argument("--stub", action="store_true",
+                    help="harness self-test on CPU: gloo, a trivial step instead of the encode (tests only)")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(x: torch.Tensor, rate: float):
-    """The reference sw/ encoder (compiled in place from /root/reference into oracle/_ref) on this host's cores.
-    sw/ only has a 2-D layout (sw/src/zfp.c:12-24), so the same bucket bytes are viewed as 16384 x 16384 and coded
-    with the same expert params sw/ would get for rate 16 in 2-D (minbits = maxbits = 256). Falls back to the 1-D
-    restatement (oracle port) when oracle/_ref is absent."""
-    import ctypes as C
+# ------------------------------------------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
-    import numpy as np
 
-    from oracle import oracle as O
+def launch(args) -> int:
+    """N > 1 without a torchrun environment: start N ranks (one process per GPU) through torchrun on 127.0.0.1 and
+    return its exit code. Called before anything initialises HIP in this process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["GCOW_BENCH_LAUNCHER"] = "self"
+    return subprocess.call(cmd, env=env)
 
-    a = x.detach().cpu().numpy()
-    R = O.ref()
-    if R is not None:
-        side = int(round(a.size ** 0.5))
-        rows = a.size // side
-        a2 = a[: rows * side].reshape(rows, side)
-        p = O.rate(rate, 2)
-        out = np.zeros(O.max_words(a2.shape, p) + 4, np.uint64)
-        t0 = time.perf_counter()
-        R.gcow_ref_compress_2d(a2.ctypes.data_as(C.POINTER(C.c_float)), side, rows, *p.tuple(),
-                               out.ctypes.data_as(C.POINTER(C.c_uint64)), out.nbytes)
-        dt = time.perf_counter() - t0
-        kind, sample = "reference", "sw/ zfp_compress (g++ -O2) on the full bucket viewed as %dx%d fp32, fixed rate %g " \
-                                    "(minbits=maxbits=%d), 1 thread" % (rows, side, rate, p.maxbits)
-        cores = 1
-    else:
-        p = O.rate(rate, 1)
-        t0 = time.perf_counter()
-        O.compress(a, p)
-        dt = time.perf_counter() - t0
-        kind, sample = "port", "oracle C restatement, full bucket 1-D fixed rate %g, 1 thread" % rate
-        cores = 1
-    return {"value": round(a.nbytes / dt / 2 ** 30, 4), "unit": "GiB/s", "cores": cores, "kind": kind,
-            "sample": sample, "seconds": round(dt, 3), "cpu": platform.processor() or platform.machine()}
+
+# ------------------------------------------------------------------------------------------------------ timing
+class Ctx:
+    def __init__(self, args):
+        self.args = args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.stub = args.stub
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if self.stub:
+                dist.init_process_group("gloo")
+            else:
+                torch.cuda.set_device(self.local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+        self.dev = torch.device("cpu") if self.stub else torch.device("cuda", self.local)
+        if not self.stub:
+            torch.cuda.set_device(self.dev)
+
+    def sync(self):
+        if not self.stub:
+            torch.cuda.synchronize(self.dev)
+
+    def barrier(self, group=None):
+        if self.world > 1:
+            dist.barrier(group=group)
+
+    def max_over_ranks(self, vals, group=None):
+        if self.world == 1:
+            return list(vals)
+        t = torch.tensor(list(vals), dtype=torch.float64, device=self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        return t.tolist()
+
+
+def timed(ctx: Ctx, step, warmup: int, steps: int, group=None, stream=None):
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize on both sides. Returns (wall ms per
+    step, per-step kernel ms from HIP events on `stream` -- [] in stub mode)."""
+    for _ in range(warmup):
+        step()
+    ctx.sync()
+    ctx.barrier(group)
+    ctx.sync()
+    evs = []
+    if not ctx.stub:
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    t0 = time.perf_counter()
+    if evs:
+        evs[0].record(stream)
+    for i in range(steps):
+        step()
+        if evs:
+            evs[i + 1].record(stream)
+    ctx.sync()
+    ctx.barrier(group)
+    ctx.sync()
+    wall = (time.perf_counter() - t0) * 1e3 / steps
+    per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if evs else []
+    return wall, per
+
+
+def gib(nbytes: float, ms: float) -> float:
+    return nbytes / (ms / 1e3) / 2 ** 30
+
+
+def roof(read_bytes: float, write_bytes: float, ms: float, kernel: str) -> dict:
+    a = read_bytes / (ms / 1e3) / 1e9
+    arw = (read_bytes + write_bytes) / (ms / 1e3) / 1e9
+    return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(a / HBM_PEAK_GBPS, 4), "achieved_read_write": round(arw, 1),
+            "frac_read_write": round(arw / HBM_PEAK_GBPS, 4), "kernel": kernel, "kernel_ms": round(ms, 5),
+            "algorithmic_read_bytes": int(read_bytes), "algorithmic_write_bytes": int(write_bytes)}
 
 
 def load_pmc_traffic(kernel_substr: str, workload: str):
-    """HBM bytes per launch from a committed rocprofv3 --pmc pass (profiles/*pmc_traffic.json), or None."""
+    """HBM bytes per launch (read + write) from a committed rocprofv3 --pmc pass: (bytes, file) or (None, None)."""
     prof = os.path.join(ROOT, "profiles")
     if not os.path.isdir(prof):
-        return None
+        return None, None
     for f in sorted(os.listdir(prof), reverse=True):
         if f.endswith("pmc_traffic.json"):
             try:
@@ -93,140 +169,447 @@ def load_pmc_traffic(kernel_substr: str, workload: str):
             except Exception:
                 continue
             if d.get("workload") == workload and kernel_substr in d.get("kernel", ""):
-                return d.get("hbm_bytes_per_launch")
-    return None
+                return d.get("hbm_bytes_per_launch"), "profiles/" + f
+    return None, None
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+# ------------------------------------------------------------------------------------------------------ oracle checks
+def _u64(t: torch.Tensor):
+    import numpy as np
+    return t.contiguous().cpu().numpy().view(np.uint64)
+
+
+def bits_at(words, off: int, nbits: int):
+    """nbits bits of a uint64 word array starting at bit off, as ceil(nbits / 64) words (LSB-first)."""
+    import numpy as np
+    nw = (nbits + 63) // 64
+    w = np.concatenate([words, np.zeros(2, np.uint64)])
+    i, sh = off // 64, off % 64
+    out = w[i:i + nw + 1].copy()
+    if sh:
+        out = (out[:nw] >> np.uint64(sh)) | (out[1:nw + 1] << np.uint64(64 - sh))
+    else:
+        out = out[:nw]
+    if nbits % 64:
+        out[-1] &= np.uint64((1 << (nbits % 64)) - 1)
+    return out
+
+
+def check_fixed_gathered(full: torch.Tensor, world: int, n: int, p, samples: int = 1 << 16) -> bool:
+    """Rank 0: for every shard r, regenerate r's input, oracle-encode a sampled range (the shard's start and a
+    16-block-aligned interior offset) and compare it with the gathered stream's words at that block."""
+    import numpy as np
+
+    from gcow_amd import codec
+    from oracle import oracle as O
+    op = O.expert(*p.tuple())
+    y = torch.empty(n, dtype=torch.float32, device=full.device)
+    rng = np.random.default_rng(7)
+    ok = True
+    nb = n // 4
+    for r in range(world):
+        codec.fill_normal(y, 1e-3, seed=SEED + r, inject=True)
+        for off in (0, int(rng.integers(0, (n - samples) // 64)) * 64):
+            a = y[off:off + samples].cpu().numpy()
+            w, bits = O.compress(a, op)
+            b0 = r * nb + off // 4
+            got = bits_at(_u64(full[(b0 * p.maxbits) // 64:(b0 * p.maxbits + bits) // 64 + 2]),
+                          (b0 * p.maxbits) % 64, bits)
+            ok = ok and got.tobytes() == w.tobytes()
+    return ok
+
+
+# ------------------------------------------------------------------------------------------------------ legs
+def leg_c4_exchange(ctx, enc, x, p, n, out_bytes):
+    from gcow_amd import dist as gdist
+    nb = n // 4
+    res = {}
+
+    def step():
+        e = enc(x)
+        res["full"] = gdist.allgather_fixed(e.words, nb, p.maxbits)
+
+    reps = max(3, ctx.args.steps // 4)
+    ms, _ = timed(ctx, step, 2, reps)
+    ms = ctx.max_over_ranks([ms])[0]
+    full = res.pop("full")
+    ok = check_fixed_gathered(full, ctx.world, n, p) if ctx.rank == 0 else None
+    d = {"ms_per_step": round(ms, 4), "GiBps_input": round(gib(ctx.world * n * 4, ms), 2),
+         "gathered_bytes_per_rank": int(full.numel() * 8),
+         "allgather_GBps_per_rank_ingress": round((ctx.world - 1) * out_bytes / (ms / 1e3) / 1e9, 1),
+         "gathered_stream_matches_oracle": ok,
+         "oracle_check": "every shard: its first 64 Ki values and a random interior 64 Ki-value range re-encoded by "
+                         "the oracle, compared with the gathered stream at that block"}
+    del full
+    return d
+
+
+def leg_subgroups(ctx, p, n):
+    """The 1/2/4/.. curve inside the N-rank job: k-rank sub-communicators over the first k ranks (dist.new_group),
+    members encode their own 256 Mi shard then all-gather the compressed shards within the subgroup."""
+    from gcow_amd import codec
+    from gcow_amd import dist as gdist
+    ks = [k for k in (1, 2, 4, 8, 16, 32) if k < ctx.world] + [ctx.world]
+    groups = {k: (dist.new_group(list(range(k))) if k < ctx.world else None) for k in ks}
+    x = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+    codec.fill_normal(x, 1e-3, seed=SEED + ctx.rank, inject=True)
+    enc = codec.Encoder((n,), torch.float32, p, ctx.dev)
+    nb = n // 4
+    curve = []
+    for k in ks:
+        member = ctx.rank < k
+        e_ms = a_ms = 0.0
+        if member:
+            g = groups[k]
+            e_ms, _ = timed(ctx, lambda: enc(x), 3, 10, group=g)
+            res = {}
+
+            def step():
+                e = enc(x)
+                res["f"] = gdist.allgather_fixed(e.words, nb, p.maxbits, group=g)
+
+            a_ms, _ = timed(ctx, step, 1, 4, group=g)
+            res.clear()
+        ctx.barrier()
+        e_ms, a_ms = ctx.max_over_ranks([e_ms, a_ms])
+        curve.append({"k": k, "encode_ms": round(e_ms, 4), "encode_GiBps": round(gib(k * n * 4, e_ms), 2),
+                      "encode_allgather_ms": round(a_ms, 4)})
+    del x, enc
+    return curve
+
+
+def leg_strong(ctx, p, total_values):
+    """C4 strong scaling: one total_values bucket split over k = 1, 2, 4, .. ranks (each member encodes
+    total/k values; all-gather of the compressed shards within the k-rank subgroup)."""
+    from gcow_amd import codec
+    from gcow_amd import dist as gdist
+    ks = [k for k in (1, 2, 4, 8, 16, 32) if k < ctx.world] + [ctx.world]
+    out = []
+    for k in ks:
+        g = dist.new_group(list(range(k))) if k < ctx.world else None
+        member = ctx.rank < k
+        e_ms = a_ms = 0.0
+        if member:
+            m = total_values // k // 64 * 64
+            x = torch.empty(m, dtype=torch.float32, device=ctx.dev)
+            codec.fill_normal(x, 1e-3, seed=SEED + 1000 + ctx.rank, inject=True)
+            enc = codec.Encoder((m,), torch.float32, p, ctx.dev)
+            e_ms, _ = timed(ctx, lambda: enc(x), 3, 10, group=g)
+            res = {}
+
+            def step():
+                e = enc(x)
+                res["f"] = gdist.allgather_fixed(e.words, m // 4, p.maxbits, group=g)
+
+            a_ms, _ = timed(ctx, step, 1, 3, group=g)
+            res.clear()
+            del x, enc
+            torch.cuda.empty_cache()
+        ctx.barrier()
+        e_ms, a_ms = ctx.max_over_ranks([e_ms, a_ms])
+        out.append({"k": k, "values_per_rank": total_values // k, "encode_ms": round(e_ms, 4),
+                    "encode_GiBps": round(gib(total_values * 4, e_ms), 2), "encode_allgather_ms": round(a_ms, 4)})
+    return {"bucket_bytes": total_values * 4, "curve": out}
+
+
+def leg_c5_sharded(ctx, n):
+    """C5 at N ranks: each rank encodes its own 256 Mi bf16 shard at accuracy 1e-6, then the variable-rate exchange
+    (length all-gather, padded stream all-gather, one-launch stitch). Rank 0 checks every shard's first 64 Ki values
+    against the oracle at the shard's stitched bit offset, and the total bit count against the per-shard sum."""
+    import numpy as np
+
+    from gcow_amd import codec
+    from gcow_amd import dist as gdist
+    p = codec.accuracy(1e-6)
+    x32 = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+    codec.fill_normal(x32, 1e-3, seed=SEED + ctx.rank, inject=True)
+    xb = x32.to(torch.bfloat16)
+    del x32
+    enc = codec.Encoder((n,), torch.bfloat16, p, ctx.dev)
+    e_ms, _ = timed(ctx, lambda: enc(xb), 3, 10)
+    res = {}
+
+    def step():
+        e = enc(xb)
+        res["o"] = gdist.allgather_variable(e.words, e.bits_dev)
+
+    a_ms, _ = timed(ctx, step, 1, 4)
+    e_ms, a_ms = ctx.max_over_ranks([e_ms, a_ms])
+    words, total = res.pop("o")
+    lens = gdist.gather_lengths(enc.bits_dev, ctx.dev)[1]
+    ok = None
+    if ctx.rank == 0:
+        from oracle import oracle as O
+        op = O.expert(*p.tuple())
+        ok = total == sum(lens)
+        y = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+        off = 0
+        for r in range(ctx.world):
+            codec.fill_normal(y, 1e-3, seed=SEED + r, inject=True)
+            a = y[: 1 << 16].to(torch.bfloat16).cpu().view(torch.int16).numpy().view(np.uint16)
+            w, b = O.compress(a, op)
+            got = bits_at(_u64(words[off // 64:(off + b) // 64 + 2]), off % 64, b)
+            ok = ok and got.tobytes() == w.tobytes()
+            off += lens[r]
+        del y
+    del xb, enc, words
+    return {"values_per_rank": n, "dtype": "bf16", "mode": "accuracy 1e-6",
+            "encode_ms": round(e_ms, 4), "encode_GiBps_input": round(gib(ctx.world * n * 2, e_ms), 2),
+            "encode_exchange_ms": round(a_ms, 4), "compressed_bits_total": int(total),
+            "stitched_stream_matches_oracle": ok}
+
+
+def leg_host_e2e(ctx, enc, x, p, n, in_bytes, out_bytes):
+    from gcow_amd import codec
+    h_in = x.cpu().pin_memory()
+    h_out = torch.empty(int(out_bytes // 8) + 2, dtype=torch.int64, pin_memory=True)
+    nwo = int(out_bytes // 8)
+
+    def seq():
+        x.copy_(h_in, non_blocking=True)
+        e = enc(x)
+        h_out[:nwo].copy_(e.words[:nwo], non_blocking=True)
+
+    h_ms, _ = timed(ctx, seq, 2, 5)
+    henc = codec.HostEncoder(n, torch.float32, p, chunks=8, device=ctx.dev)
+    o_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 2, 5)
+    return {"ms_per_step": round(h_ms, 3), "GiBps_input": round(gib(in_bytes, h_ms), 2),
+            "overlapped_ms_per_step": round(o_ms, 3), "overlapped_GiBps_input": round(gib(in_bytes, o_ms), 2),
+            "note": "pinned hipMemcpyAsync H2D + encode + D2H, PCIe-inclusive (not `value`); overlapped = 8 chunks, "
+                    "H2D / encode / D2H on three streams (codec.HostEncoder)"}
+
+
+def _c3_field(dev, side=512):
+    """f = sin(6 pi x) cos(4 pi y) sin(2 pi z) + 1e-3 N(0, 1) on the [0, 1)^3 grid (z slowest)."""
+    g = torch.arange(side, device=dev, dtype=torch.float32) / side
+    f = (torch.sin(6 * math.pi * g)[None, None, :] * torch.cos(4 * math.pi * g)[None, :, None] *
+         torch.sin(2 * math.pi * g)[:, None, None])
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(SEED)
+    f += 1e-3 * torch.randn(f.shape, device=dev, generator=gen)
+    return f.contiguous()
+
+
+def leg_configs(ctx):
+    """C3 and C5 at N = 1, each with its own roofline fraction (read-only bytes = the input; read + write adds the
+    compressed bytes)."""
+    from gcow_amd import codec
+    out = {}
+    f = _c3_field(ctx.dev)
+    nbytes = f.numel() * 4
+    for name, p, stride in (("c3_512cube_rate8", codec.rate(8, 3), 0),
+                            ("c3_512cube_acc1e-3", codec.accuracy(1e-3), 1)):
+        enc = codec.Encoder(tuple(f.shape), torch.float32, p, ctx.dev, index_stride=stride)
+        st = torch.cuda.current_stream(ctx.dev)
+        e_ms, per = timed(ctx, lambda: enc(f, st), 5, 20, stream=st)
+        k_ms = sum(per) / len(per)
+        e = enc(f, st)
+        cbits = e.bits
+        back = torch.empty_like(f)
+        d_ms, dper = timed(ctx, lambda: codec.decode(e, out=back, stream=st), 5, 20, stream=st)
+        dk = sum(dper) / len(dper)
+        err = float((back - f).abs().max())
+        out[name] = {"encode_ms": round(k_ms, 4), "encode_GiBps_input": round(gib(nbytes, k_ms), 2),
+                     "decode_ms": round(dk, 4), "decode_GiBps_output": round(gib(nbytes, dk), 2),
+                     "bits_per_value": round(cbits / f.numel(), 3), "max_abs_err": err,
+                     "encode_roofline": roof(nbytes, cbits / 8, k_ms, "k_encode3d_fixed" if stride == 0 else
+                                             "k_count + k_scan_ranges + k_encode_tiles<3>"),
+                     "decode_roofline": roof(cbits / 8, nbytes, dk, "k_decode3d_fixed" if stride == 0 else
+                                             "k_decode_staged<3>")}
+        del enc, back, e
+    del f
+    torch.cuda.empty_cache()
+    n = N_VALUES
+    x32 = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+    codec.fill_normal(x32, 1e-3, seed=SEED, inject=True)
+    xb = x32.to(torch.bfloat16)
+    del x32
+    for name, tol in (("c5_bf16_acc1e-6", 1e-6), ("c5_bf16_acc1e-3", 1e-3)):
+        p = codec.accuracy(tol)
+        enc = codec.Encoder((n,), torch.bfloat16, p, ctx.dev, index_stride=16)
+        st = torch.cuda.current_stream(ctx.dev)
+        _, per = timed(ctx, lambda: enc(xb, st), 5, 20, stream=st)
+        k_ms = sum(per) / len(per)
+        cbits = enc(xb, st).bits
+        h_in = xb.cpu().pin_memory()
+        h_out = torch.empty(codec.max_output_bytes((n,), p, torch.bfloat16) // 8 + 2, dtype=torch.int64,
+                            pin_memory=True)
+        henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=8, device=ctx.dev)
+        h_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 2, 5)
+        out[name] = {"encode_ms": round(k_ms, 4), "encode_GiBps_input": round(gib(n * 2, k_ms), 2),
+                     "bits_per_value": round(cbits / n, 3),
+                     "encode_roofline": roof(n * 2, cbits / 8, k_ms, "k_count1d_var + k_scan_ranges + k_encode1d_var"),
+                     "host_path_ms": round(h_ms, 3), "host_path_GiBps_input": round(gib(n * 2, h_ms), 2),
+                     "host_path_note": "pinned bf16 H2D + encode + D2H of the stream, 8 overlapped chunks (PCIe-bound)"}
+        del enc, h_in, h_out, henc
+    del xb
+    torch.cuda.empty_cache()
+    return out
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(x: torch.Tensor, rate: float) -> dict:
+    """The reference's CPU path on this host's cores, on bounded samples of the same bucket, best of 5:
+      reference  sw/ zfp_compress compiled from /root/reference/sw/src (oracle/_ref, g++ -O3 -march=x86-64-v3), one
+                 thread (sw/ has no threads), 2-D (its only layout: sw/src/zfp.c:12-24) on 64 Mi values viewed 8192^2;
+      port_1t    the oracle restatement (gcc -O3 -march=native, built here) on the same 1-D rate-16 config, 1 thread,
+                 32 Mi values;
+      port_mt    the same on the whole 256 Mi bucket with T threads over block-aligned shards + a serial bit stitch.
+    The headline is `reference`; without oracle/_ref it is port_1t and `reference_missing` says why."""
+    import ctypes as C
+
+    import numpy as np
+
+    from oracle import oracle as O
+    a = x.detach().cpu().numpy()
+    legs = {}
+
+    def best(fn, reps=5):
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+
+    R = O.ref()
+    missing = None
+    if R is not None:
+        side = 8192
+        a2 = np.ascontiguousarray(a[: side * side].reshape(side, side))
+        p = O.rate(rate, 2)
+        out = np.zeros(O.max_words(a2.shape, p) + 4, np.uint64)
+        dt = best(lambda: R.gcow_ref_compress_2d(a2.ctypes.data_as(C.POINTER(C.c_float)), side, side, *p.tuple(),
+                                                   out.ctypes.data_as(C.POINTER(C.c_uint64)), out.nbytes))
+        legs["reference"] = {"value": round(a2.nbytes / dt / 2 ** 30, 4), "cores": 1, "seconds_best": round(dt, 3),
+                             "sample": "sw/ zfp_compress, 8192 x 8192 fp32 view of the bucket's first 64 Mi values, "
+                                       "fixed rate %g (2-D: minbits = maxbits = %d), 1 thread" % (rate, p.maxbits)}
+    else:
+        missing = ("oracle/_ref/libgcow_ref.so absent: it is compiled from /root/reference/sw/src by oracle/Makefile "
+                   "(make -C oracle ref) in the build container and travels with the tree")
+        print("bench.py: WARNING: " + missing, file=sys.stderr)
+    L, flags = O.native_lib()
+    p1 = O.rate(rate, 1)
+    s1 = np.ascontiguousarray(a[: 32 << 20])
+    dt = best(lambda: O.compress(s1, p1, L=L))
+    legs["port_1t"] = {"value": round(s1.nbytes / dt / 2 ** 30, 4), "cores": 1, "seconds_best": round(dt, 3),
+                       "sample": "oracle restatement (%s), 1-D fixed rate %g, first 32 Mi values" % (flags, rate)}
+    T = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+    T = max(1, min(T, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else T))
+    dt = best(lambda: O.compress(a, p1, threads=T, L=L))
+    legs["port_mt"] = {"value": round(a.nbytes / dt / 2 ** 30, 4), "cores": T, "seconds_best": round(dt, 3),
+                       "sample": "oracle restatement (%s), 1-D fixed rate %g, whole 256 Mi bucket, %d threads over "
+                                 "block-aligned shards + serial bit stitch" % (flags, rate, T)}
+    head = legs.get("reference") or legs["port_1t"]
+    d = {"value": head["value"], "unit": "GiB/s", "cores": head["cores"],
+         "kind": "reference" if "reference" in legs else "port", "sample": head["sample"],
+         "cpu": _cpu_model(), "host_cpus": os.cpu_count(), "best_of": 5, "legs": legs}
+    if missing:
+        d["reference_missing"] = missing
+    return d
+
+
+# ------------------------------------------------------------------------------------------------------ main
+def stub_worker(ctx: Ctx):
+    """Harness self-test (tests/test_bench_launcher.py): the same timing / max-over-ranks / JSON path with a trivial
+    CPU step."""
+    t = torch.ones(1 << 12)
+    wall, _ = timed(ctx, lambda: t.sum(), ctx.args.warmup, ctx.args.steps)
+    wall = ctx.max_over_ranks([wall])[0]
+    me = [ctx.rank, ctx.local, ctx.world, os.environ.get("GCOW_BENCH_LAUNCHER", "torchrun")]
+    ranks = [None] * ctx.world
+    if ctx.world > 1:
+        dist.all_gather_object(ranks, me)
+    else:
+        ranks = [me]
+    if ctx.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(gib(ctx.world * ctx.args.values * 4, wall), 3),
+                          "unit": "GiB/s", "n_gpus": ctx.world, "steps": ctx.args.steps, "warmup": ctx.args.warmup,
+                          "ms_per_step": round(wall, 5), "data": "stub", "ranks": ranks}), flush=True)
+
+
+def worker(args):
+    ctx = Ctx(args)
+    if ctx.stub:
+        stub_worker(ctx)
+        if ctx.world > 1:
+            dist.destroy_process_group()
+        return
+    from gcow_amd import codec  # after the device is set: libgcow.so shares torch's HIP runtime
 
     n = args.values
-    x = torch.empty(n, dtype=torch.float32, device=dev)
-    codec.fill_normal(x, 1e-3, seed=0x67636F77 + rank, inject=True)
+    world, rank = ctx.world, ctx.rank
+    x = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+    codec.fill_normal(x, 1e-3, seed=SEED + rank, inject=True)
     p = codec.rate(args.rate, 1)
-    enc = codec.Encoder((n,), torch.float32, p, dev)
-    stream = torch.cuda.current_stream(dev)
-
-    for _ in range(args.warmup):
-        enc(x, stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        enc(x, stream)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel per step on this stream: HIP-event kernel time
-    step_ms = wall * 1e3 / args.steps
-    if world > 1:
-        t = torch.tensor([step_ms, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        step_ms, kern_ms = t.tolist()
+    enc = codec.Encoder((n,), torch.float32, p, ctx.dev)
+    stream = torch.cuda.current_stream(ctx.dev)
+    step_ms, per = timed(ctx, lambda: enc(x, stream), args.warmup, args.steps, stream=stream)
+    kern_ms = sum(per) / len(per)
+    step_ms, kern_ms = ctx.max_over_ranks([step_ms, kern_ms])
 
     in_bytes = n * 4
     out_bytes = n * args.rate / 8
-    value = world * in_bytes / (step_ms / 1e3) / 2 ** 30
+    value = world * gib(in_bytes, step_ms)
     workload = "c2_1d_fp32_fixed_rate%g_%dMi_per_gpu" % (args.rate, n // (1 << 20))
-    achieved = (in_bytes + out_bytes) / (kern_ms / 1e3) / 1e9
+    kname = "k_encode_fixed1d_np"
+    roofline = roof(in_bytes, out_bytes, kern_ms, kname)
+    traffic, src = load_pmc_traffic(kname, workload)
+    roofline["traffic"] = traffic
+    roofline["traffic_source"] = (src + " (rocprofv3 --pmc TCC read + write bytes per launch, same kernel and "
+                                  "workload; not measured in this run)") if src else None
+    extra = {"per_launch_ms": {"first": round(per[0], 4), "median": round(statistics.median(per), 4),
+                               "min": round(min(per), 4), "max": round(max(per), 4)}}
+    # the same kernel once the clock has settled under load (>= 0.25 s of back-to-back launches)
+    t_end = time.perf_counter() + 0.25
+    while time.perf_counter() < t_end:
+        for _ in range(50):
+            enc(x, stream)
+        ctx.sync()
+    s_ms, sper = timed(ctx, lambda: enc(x, stream), 0, 200, stream=stream)
+    sk = sum(sper) / len(sper)
+    s_ms, sk = ctx.max_over_ranks([s_ms, sk])
+    extra["steady_state"] = {"ms_per_step": round(s_ms, 5), "GiBps": round(world * gib(in_bytes, s_ms), 2),
+                             "kernel_ms": round(sk, 5), "frac": round(in_bytes / (sk / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                             "frac_read_write": round((in_bytes + out_bytes) / (sk / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}
 
-    extra = {}
-    # RCCL all-gather of the compressed shards (C4 exchange step), timed on its own
-    if world > 1 and not args.no_allgather:
-        from gcow_amd import dist as gdist
-        nb = n // 4
-        e = enc(x, stream)
-        for _ in range(2):
-            full = gdist.allgather_fixed(e.words, nb, p.maxbits)
-        torch.cuda.synchronize()
-        dist.barrier()
-        ta = time.perf_counter()
-        reps = max(3, args.steps // 4)
-        for _ in range(reps):
-            e = enc(x, stream)
-            full = gdist.allgather_fixed(e.words, nb, p.maxbits)
-        torch.cuda.synchronize()
-        dist.barrier()
-        ag_ms = (time.perf_counter() - ta) * 1e3 / reps
-        t = torch.tensor([ag_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ag_ms = t.item()
-        # parity of the gathered single stream: rank 0 re-encodes every rank's shard locally and compares
-        ok = True
-        if rank == 0:
-            y = torch.empty_like(x)
-            shard_words = nb * p.maxbits // 64
-            for r in range(world):
-                codec.fill_normal(y, 1e-3, seed=0x67636F77 + r, inject=True)
-                er = codec.encode(y, p)
-                ok = ok and bool(torch.equal(er.words[:shard_words], full[r * shard_words:(r + 1) * shard_words]))
-            del y
-        extra["encode_allgather"] = {"ms_per_step": round(ag_ms, 4),
-                                     "GiBps_input": round(world * in_bytes / (ag_ms / 1e3) / 2 ** 30, 2),
-                                     "gathered_bytes_per_rank": int(full.numel() * 8),
-                                     "gathered_stream_equals_single_gpu_encode": ok}
-        del full
-
-    if rank == 0 and world == 1 and not args.no_host_e2e:
-        # path that starts and ends in host memory: pinned H2D of the bucket + encode + D2H of the stream
-        h_in = x.cpu().pin_memory()
-        h_out = torch.empty(int(out_bytes // 8), dtype=torch.int64, pin_memory=True)
-        for _ in range(2):
-            x.copy_(h_in, non_blocking=True)
-            e = enc(x, stream)
-            h_out.copy_(e.words[: h_out.numel()], non_blocking=True)
-        torch.cuda.synchronize()
-        th = time.perf_counter()
-        reps = 5
-        for _ in range(reps):
-            x.copy_(h_in, non_blocking=True)
-            e = enc(x, stream)
-            h_out.copy_(e.words[: h_out.numel()], non_blocking=True)
-        torch.cuda.synchronize()
-        h_ms = (time.perf_counter() - th) * 1e3 / reps
-        henc = codec.HostEncoder(n, torch.float32, p, chunks=8, device=dev)
-        for _ in range(2):
-            henc(h_in, h_out)
-        th = time.perf_counter()
-        for _ in range(reps):
-            henc(h_in, h_out)
-        o_ms = (time.perf_counter() - th) * 1e3 / reps
-        extra["host_e2e"] = {"ms_per_step": round(h_ms, 3), "GiBps_input": round(in_bytes / (h_ms / 1e3) / 2 ** 30, 2),
-                             "overlapped_ms_per_step": round(o_ms, 3),
-                             "overlapped_GiBps_input": round(in_bytes / (o_ms / 1e3) / 2 ** 30, 2),
-                             "note": "pinned hipMemcpyAsync H2D + encode + D2H, PCIe-inclusive (not `value`); "
-                                     "overlapped = 8 chunks, H2D / encode / D2H on three streams (codec.HostEncoder)"}
-        del h_in, h_out
+    if not args.no_extras:
+        if world > 1:
+            extra["encode_allgather"] = leg_c4_exchange(ctx, lambda t: enc(t, stream), x, p, n, out_bytes)
+            torch.cuda.empty_cache()
+            extra["subgroups"] = leg_subgroups(ctx, p, n)
+            torch.cuda.empty_cache()
+            del x, enc
+            torch.cuda.empty_cache()
+            extra["strong"] = leg_strong(ctx, p, int(args.strong_gib * (1 << 30)) // 4)
+            extra["c5_sharded"] = leg_c5_sharded(ctx, N_VALUES)
+        else:
+            extra["host_e2e"] = leg_host_e2e(ctx, lambda t: enc(t, stream), x, p, n, in_bytes, out_bytes)
+            extra["configs"] = leg_configs(ctx)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
+            if "x" not in locals():
+                x = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+                codec.fill_normal(x, 1e-3, seed=SEED, inject=True)
             cpu = cpu_baseline(x, args.rate)
         except Exception as ex:  # the GPU measurement stands on its own
             cpu = {"error": repr(ex)}
+            print("bench.py: cpu_baseline failed: %r" % (ex,), file=sys.stderr)
 
     if rank == 0:
-        kname = "k_encode_fixed1d_np"
-        traffic = load_pmc_traffic(kname, workload)
         line = {
-            "metric": "GiB/s device-resident fp32->ZFP encode, 256Mi-float bucket, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -240,18 +623,22 @@ def main():
             "data": "synthetic: N(0,1e-3) fp32 with 1/64 zero, 1/4096 tiny (INT_MIN path), 1/4096 subnormal blocks",
             "config": {"workload": workload, "values_per_gpu": n, "layout": "1-D contiguous, 4-value blocks",
                        "mode": "fixed-rate", "rate_bits_per_value": args.rate, "minbits": p.minbits,
-                       "maxbits": p.maxbits, "bucket_bytes_total": world * in_bytes},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
-                         "kernel": kname, "kernel_ms": round(kern_ms, 5),
-                         "algorithmic_bytes_per_launch": int(in_bytes + out_bytes)},
+                       "maxbits": p.maxbits, "bucket_bytes_total": world * in_bytes,
+                       "launcher": os.environ.get("GCOW_BENCH_LAUNCHER", "torchrun" if world > 1 else "none")},
+            "roofline": roofline,
             "cpu_baseline": cpu,
         }
         line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main(argv=None):
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
+    worker(args)
 
 
 if __name__ == "__main__":

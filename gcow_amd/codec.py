@@ -68,6 +68,10 @@ def field_of(t: torch.Tensor, dims: int | None = None) -> ZfpInput:
     names_n = ["nx", "ny", "nz", "nw"]
     names_s = ["sx", "sy", "sz", "sw"]
     for i in range(t.dim()):
+        if st[i] == 0 and shp[i] > 1:
+            # an expanded / broadcast view: the ABI reads stride 0 as "dense" (sw/src/zfp.c:37-38), which would walk
+            # past the tensor's storage
+            raise GcowError("stride 0 on a dimension of size %d (expanded view): pass t.contiguous()" % shp[i])
         setattr(f, names_n[i], int(shp[i]))
         setattr(f, names_s[i], int(st[i]))
     return f
@@ -210,6 +214,33 @@ def stitch(dst: torch.Tensor, dst_bit_offset: int, src: torch.Tensor, src_bits: 
           "gcow_stitch_device")
 
 
+def stitch_shards(dst: torch.Tensor, src: torch.Tensor, shard_words: int, lens: torch.Tensor, stream=None):
+    """Concatenate len(lens) shard streams (lens: int64 device tensor of bit counts; shard r at src[r * shard_words:])
+    bit-exactly into dst (every word of dst is written; one launch, no host sync)."""
+    n = lens.numel()
+    if src.numel() < n * shard_words:
+        raise GcowError("stitch_shards: src holds %d words, %d shards of %d expected" % (src.numel(), n, shard_words))
+    check(load().gcow_stitch_shards_device(dst.data_ptr(), dst.numel(), src.data_ptr(), shard_words, lens.data_ptr(),
+                                           n, _stream_ptr(stream)), "gcow_stitch_shards_device")
+    return dst
+
+
+def decode_mean(streams: torch.Tensor, stream_words: int, nstreams: int, n: int, params: GcowParams,
+                index: torch.Tensor | None = None, index_words: int = 0, index_stride: int = 0,
+                out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """Mean of the decodes of nstreams 1-D streams of n values (stream r at streams[r * stream_words:], 2 readable
+    words after the last one), accumulated in rank order in fp32 (gcow_decode_mean_device): one launch."""
+    if streams.numel() < nstreams * stream_words + 2:
+        raise GcowError("decode_mean: the stream buffer needs 2 words of padding after the last stream")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=streams.device)
+    f = field_of(out)
+    check(load().gcow_decode_mean_device(C.byref(f), C.byref(params), streams.data_ptr(), stream_words, nstreams,
+                                         index.data_ptr() if index is not None else None, index_words, index_stride,
+                                         _stream_ptr(stream)), "gcow_decode_mean_device")
+    return out
+
+
 def fill_normal(out: torch.Tensor, sigma: float = 1e-3, seed: int = 0x67636F77, inject: bool = True, stream=None):
     """Deterministic synthetic gradient bucket on the device (SURVEY 8(d) distribution)."""
     assert out.dtype == torch.float32 and out.is_cuda and out.is_contiguous()
@@ -322,7 +353,13 @@ class HostEncoder:
         self.device = torch.device(device or "cuda")
         self.fixed = is_fixed(params)
         nb = (self.n + 3) // 4
-        per = max(16, ((nb + chunks - 1) // chunks + 15) // 16 * 16)  # 16-block multiples: 64-bit aligned chunks
+        # chunks of a multiple of 16 blocks; fixed rate also needs every chunk to start on a 64-bit stream word
+        # (written at a byte offset as its own stream): blocks * maxbits % 64 == 0
+        align = 16
+        if self.fixed:
+            g = 64 // math.gcd(int(params.maxbits), 64)
+            align = align * g // math.gcd(align, g)
+        per = max(align, ((nb + chunks - 1) // chunks + align - 1) // align * align)
         self.bounds = []
         b = 0
         while b < nb:

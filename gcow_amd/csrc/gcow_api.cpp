@@ -224,7 +224,7 @@ gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void
   if (F.nblocks == 0) return GCOW_OK;
   const bool fixed = p->minbits == p->maxbits;
   if (fixed && F.dims == 1 && F.vec && (p->maxbits == 64 || p->maxbits == 32) && p->maxprec >= 32 &&
-      p->minexp <= -154 && base_bits % 32 == 0 && !d_end && !getenv("GCOW_GENERIC_DECODE")) {
+      p->minexp <= -154 && base_bits % 32 == 0 && !d_end) {
     GCOW_HIP(gcow::launch_decode_fixed1d(F, P(*p), (const uint64_t*)d_in, base_bits, stream));
     return GCOW_OK;
   }
@@ -254,7 +254,7 @@ gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void
     chunk = F.nblocks;  // no index: one sequential lane
     nchunks = 1;
   }
-  if (!fixed && F.dims == 1 && F.vec && p->minbits <= 1 && p->maxbits >= 160 && !getenv("GCOW_GENERIC_DECODE")) {
+  if (!fixed && F.dims == 1 && F.vec && p->minbits <= 1 && p->maxbits >= 160) {
     GCOW_HIP(gcow::launch_decode1d_var(F, P(*p), (const uint64_t*)d_in, in_bytes / 8, d_index, chunk, nchunks,
                                        base_bits, d_end, stream));
     return GCOW_OK;
@@ -285,6 +285,8 @@ struct OutState {
   gcow_params params{};
   uint32_t dims = 0;
   uint64_t nblocks = 0;
+  uint64_t words = 0;
+  uint64_t fp[64] = {};  // fingerprint() of the caller's stream when the cache was filled
 };
 
 std::mutex g_mu;
@@ -330,6 +332,44 @@ hipError_t grow(void** p, size_t* cap, size_t need)
 }
 
 gcow_params params_of(const zfp_output* o) { return gcow_params{o->minbits, o->maxbits, o->maxprec, o->minexp}; }
+
+// Element offsets [lo, hi] that a (possibly strided, possibly negatively strided) field touches, relative to its
+// data pointer, with sw/'s stride defaults (sw/src/zfp.c:37-38: sx = 1, sy = nx, ...).
+void field_span(const zfp_input* in, ptrdiff_t* lo, ptrdiff_t* hi)
+{
+  const uint32_t d = dims_of(in);
+  const size_t n[4] = {in->nx, d > 1 ? in->ny : 1, d > 2 ? in->nz : 1, d > 3 ? in->nw : 1};
+  const ptrdiff_t s[4] = {in->sx ? in->sx : 1, d > 1 ? (in->sy ? in->sy : (ptrdiff_t)in->nx) : 0,
+                          d > 2 ? (in->sz ? in->sz : (ptrdiff_t)(in->nx * in->ny)) : 0,
+                          d > 3 ? (in->sw ? in->sw : (ptrdiff_t)(in->nx * in->ny * in->nz)) : 0};
+  *lo = *hi = 0;
+  for (int k = 0; k < 4; k++) {
+    const ptrdiff_t e = (ptrdiff_t)(n[k] ? n[k] - 1 : 0) * s[k];
+    if (e < 0) *lo += e;
+    else *hi += e;
+  }
+}
+
+bool strided(const zfp_input* in) { return in->sx || in->sy || in->sz || in->sw; }
+
+// Sampled fingerprint of a stream's first `words` words (host or device): the first, the last and 62 evenly spaced
+// words. zfp_decompress reuses the device copy left by zfp_compress only while this still matches, so a caller that
+// rewrote the host buffer in between (read another stream into it, say) is decoded from its new contents.
+constexpr int kFingerprint = 64;
+bool fingerprint(const uint64_t* w, uint64_t words, bool dev, uint64_t* fp)
+{
+  std::memset(fp, 0, kFingerprint * 8);
+  if (!words) return true;
+  const uint64_t step = words > 1 ? std::max<uint64_t>((words - 1) / (kFingerprint - 1), 1) : 1;
+  const uint64_t cnt = std::min<uint64_t>(words > 1 ? (words - 1) / step + 1 : 1, kFingerprint - 1);
+  if (!dev) {
+    for (uint64_t i = 0; i < cnt; i++) fp[i] = w[i * step];
+    fp[kFingerprint - 1] = w[words - 1];
+    return true;
+  }
+  if (hipMemcpy2D(fp, 8, w, step * 8, 8, cnt, hipMemcpyDeviceToHost) != hipSuccess) return false;
+  return hipMemcpy(fp + kFingerprint - 1, w + words - 1, 8, hipMemcpyDeviceToHost) == hipSuccess;
+}
 
 // Host-side copy of `bits` bits from words src into stream s at its current write position (stream.c:61-92).
 void append_bits(stream* s, const uint64_t* src, uint64_t bits)
@@ -924,6 +964,37 @@ gcow_status gcow_stitch_device(uint64_t* d_dst, uint64_t dst_bit_offset, const u
   return GCOW_OK;
 }
 
+gcow_status gcow_stitch_shards_device(uint64_t* d_dst, uint64_t dst_words, const uint64_t* d_src, uint64_t shard_words,
+                                      const uint64_t* d_lens, uint32_t nshards, void* hip_stream)
+{
+  if (!d_dst && dst_words) return fail(GCOW_ERR_INVALID, "null destination");
+  if (nshards && (!d_src || !d_lens)) return fail(GCOW_ERR_INVALID, "null shard buffer or lengths");
+  GCOW_HIP(gcow::launch_stitch_shards(d_dst, dst_words, d_src, shard_words, d_lens, nshards, hip_stream));
+  return GCOW_OK;
+}
+
+gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p, const uint64_t* d_streams,
+                                    uint64_t stream_words, uint32_t nstreams, const uint64_t* d_index,
+                                    uint64_t index_words, uint32_t index_stride, void* hip_stream)
+{
+  gcow::FieldDesc F;
+  gcow_status st = make_field(field, F, true);
+  if (st) return st;
+  if ((st = check_params(p, 1))) return st;
+  if (F.dims != 1) return fail(GCOW_ERR_UNSUPPORTED, "decode_mean is for 1-D buckets");
+  if (!nstreams || !d_streams) return fail(GCOW_ERR_INVALID, "no streams");
+  if (p->minbits != p->maxbits) {
+    if (!(p->minbits <= 1 && p->maxbits >= 160))
+      return fail(GCOW_ERR_UNSUPPORTED, "variable-rate decode_mean needs minbits <= 1, maxbits >= 160");
+    if (!d_index || index_stride != 16 || index_words < (F.nblocks + 15) / 16)
+      return fail(GCOW_ERR_INVALID, "variable-rate decode_mean needs each stream's index (stride 16)");
+  } else if (stream_words < ((uint64_t)F.nblocks * p->maxbits + 63) / 64) {
+    return fail(GCOW_ERR_INVALID, "stream_words below one fixed-rate stream");
+  }
+  GCOW_HIP(gcow::launch_decode_mean1d(F, P(*p), d_streams, stream_words, nstreams, d_index, index_words, hip_stream));
+  return GCOW_OK;
+}
+
 gcow_status gcow_fill_normal_device(float* d_out, size_t count, double sigma, uint64_t seed, int inject,
                                     void* hip_stream)
 {
@@ -997,18 +1068,18 @@ size_t zfp_compress(zfp_output* output, const zfp_input* input)
   const bool dev_out = is_device_ptr(s->begin);
   zfp_input in2 = *input;
   if (!dev_in) {
-    // host input: stage the (densely strided) array on the device
-    if (input->sx || input->sy || input->sz) {
-      g_err = "strided host input is not supported; pass a device pointer";
-      stream_flush(s);
-      return stream_size_bytes(s);
-    }
-    if (grow(&st->d_data, &st->d_data_cap, nvals * esz) != hipSuccess ||
-        hipMemcpy(st->d_data, input->data, nvals * esz, hipMemcpyHostToDevice) != hipSuccess) {
+    // host input: stage it on the device. A strided array (sw/src/zfp.c:37-39, 45) is copied as the element span its
+    // strides touch, and keeps its strides against the device copy.
+    ptrdiff_t lo = 0, hi = (ptrdiff_t)nvals - 1;
+    if (strided(input)) field_span(input, &lo, &hi);
+    const size_t span = (size_t)(hi - lo + 1) * esz;
+    if (grow(&st->d_data, &st->d_data_cap, span) != hipSuccess ||
+        hipMemcpy(st->d_data, (const char*)input->data + lo * (ptrdiff_t)esz, span, hipMemcpyHostToDevice) !=
+            hipSuccess) {
       g_err = "H2D copy failed";
       return 0;
     }
-    in2.data = st->d_data;
+    in2.data = (char*)st->d_data - lo * (ptrdiff_t)esz;
   }
   const size_t cap = gcow_max_output_bytes(&in2, &p);
   const uint32_t stride = d == 3 ? 1 : (d == 2 ? 4 : 16);
@@ -1061,8 +1132,10 @@ size_t zfp_compress(zfp_output* output, const zfp_input* input)
     free(tmp);
     stream_flush(s);
   }
+  if (!fingerprint((const uint64_t*)s->begin, words, dev_out, st->fp)) return 0;
   st->valid = true;
   st->host_begin = s->begin;
+  st->words = words;
   st->bits = bits;
   st->index_stride = fixed ? 0 : stride;
   st->params = p;
@@ -1092,8 +1165,13 @@ size_t zfp_decompress(zfp_output* output, const zfp_input* input)
   const bool dev_out = is_device_ptr(input->data);
   const bool dev_stream = is_device_ptr(s->begin);
   const bool fixed = p.minbits == p.maxbits;
-  const bool cached = st->valid && start == 0 && st->host_begin == s->begin && st->dims == d &&
-                      st->nblocks == F.nblocks && std::memcmp(&st->params, &p, sizeof(p)) == 0;
+  bool cached = st->valid && start == 0 && st->host_begin == s->begin && st->dims == d &&
+                st->nblocks == F.nblocks && std::memcmp(&st->params, &p, sizeof(p)) == 0;
+  if (cached) {  // the caller may have rewritten its buffer since zfp_compress filled the cache
+    uint64_t fp[kFingerprint];
+    cached = fingerprint((const uint64_t*)s->begin, st->words, dev_stream, fp) &&
+             std::memcmp(fp, st->fp, sizeof(fp)) == 0;
+  }
   if (!st->d_u64 && hipMalloc((void**)&st->d_u64, 16) != hipSuccess) return 0;
   const void* d_stream;
   const uint64_t* d_index = nullptr;
@@ -1115,10 +1193,17 @@ size_t zfp_decompress(zfp_output* output, const zfp_input* input)
     d_stream = st->d_stream;
     base = start % 64;
   }
+  // host output: decode into a device copy of the element span the strides touch (dense: the array itself), whose
+  // untouched gaps are the caller's own values (sw/src/zfp.c:86-92 scatters through sx / sy)
+  ptrdiff_t lo = 0, hi = (ptrdiff_t)nvals - 1;
+  if (!dev_out && strided(input)) field_span(input, &lo, &hi);
+  const size_t span = (size_t)(hi - lo + 1) * 4;
   if (!dev_out) {
-    if (grow(&st->d_data, &st->d_data_cap, nvals * 4) != hipSuccess) return 0;
-    in2.data = st->d_data;
-    in2.sx = in2.sy = in2.sz = in2.sw = 0;
+    if (grow(&st->d_data, &st->d_data_cap, span) != hipSuccess) return 0;
+    if (strided(input) && hipMemcpy(st->d_data, (const char*)input->data + lo * 4, span, hipMemcpyHostToDevice) !=
+                              hipSuccess)
+      return 0;
+    in2.data = (char*)st->d_data - lo * 4;
   }
   if (decode_impl(&in2, &p, d_stream, d_index, stride, base, st->d_u64 + 1, nullptr) != GCOW_OK) return 0;
   uint64_t end = 0;
@@ -1128,11 +1213,7 @@ size_t zfp_decompress(zfp_output* output, const zfp_input* input)
     return 0;
   }
   if (!dev_out) {
-    if (input->sx || input->sy || input->sz) {
-      g_err = "strided host output is not supported; pass a device pointer";
-      return 0;
-    }
-    if (hipMemcpy(input->data, st->d_data, nvals * 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    if (hipMemcpy((char*)input->data + lo * 4, st->d_data, span, hipMemcpyDeviceToHost) != hipSuccess) return 0;
   } else if (hipDeviceSynchronize() != hipSuccess) {
     return 0;
   }

@@ -535,54 +535,6 @@ __device__ __forceinline__ void pipe_store(uint32_t off, pipe_v4i rs, uint64_t w
     asm volatile("buffer_store_dword %0, %1, %2, 0 offen nt" : : "v"((uint32_t)w), "v"(off), "s"(rs) : "memory");
 }
 
-// Persistent grid-stride encoder with NB rotating register buffers (prefetch depth NB): each step codes buffer k,
-// stores the block, then refills buffer k with the block NB strides ahead. In steady state the block coded next was
-// loaded NB steps ago and 2 (NB - 1) memory ops were issued after it, hence vmcnt(2 (NB - 1)). The caller keeps
-// (nfull + NB * stride) * bytes-per-block below 2^32 (chunked launches).
-template <int DT, uint32_t WB, int NB>
-__global__ __launch_bounds__(256) void k_encode_fixed1d_pipe(const void* __restrict__ in, uint32_t nfull, Params p,
-                                                             void* __restrict__ out)
-{
-  __shared__ uint32_t tab2[1280];
-#pragma unroll
-  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab5.v[t];
-  __syncthreads();
-  constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;  // input bytes per block
-  const pipe_v4i rin = buf_rsrc(in, nfull * IB), rout = buf_rsrc(out, nfull * (WB / 8));
-  const uint32_t stride = gridDim.x * 256u;
-  uint32_t b = blockIdx.x * 256u + threadIdx.x;
-  uint32_t bw = __builtin_amdgcn_readfirstlane(blockIdx.x * 256u + (threadIdx.x & ~63u));  // wave's first block
-  if (bw >= nfull) return;
-  typename PipeRow<DT>::T r[NB];
-#pragma unroll
-  for (int d = 0; d < NB; d++) r[d] = PipeRow<DT>::load((b + d * stride) * IB, rin);
-#pragma unroll
-  for (int d = 0; d < NB; d++) pipe_wait<0>(r[d]);
-  for (;;) {
-#pragma unroll
-    for (int k = 0; k < NB; k++) {
-      pipe_wait<2 * (NB - 1)>(r[k]);
-      float f[4];
-      PipeRow<DT>::unpack(r[k], f);
-      bool special;
-      uint64_t w = encode_block1d_lean5<WB>(f, tab2, special);
-      if (special) {
-        RegWriter64 rw{0ull, 0u};
-        encode_block<1>(rw, f, p);
-        w = WB == 64 ? rw.acc : (rw.acc & ((1ull << WB) - 1ull));
-      }
-      pipe_store<WB>(b * (WB / 8), rout, w);
-      r[k] = PipeRow<DT>::load((b + NB * stride) * IB, rin);
-      b += stride;
-      bw += stride;
-      if (bw >= nfull) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        return;
-      }
-    }
-  }
-}
-
 // One-shot (non-persistent) fixed-rate 1-D encoder: each lane codes U blocks 256 apart inside its workgroup's chunk
 // of 256 U blocks. All U loads are issued first (before the LDS table fill), then each block waits for its own load
 // only: with U loads followed by k stores outstanding, load k has landed once at most U - 1 operations remain
@@ -836,7 +788,7 @@ __device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uin
   const uint32_t m = max(max(a0, a1), max(a2, a3));
   special = m >= 0x7f800000u;
   const uint32_t E = special ? 150u : (m >> 23);
-  const int emax = (int)max(E, 1u) - 126;  // frexp exponent of max|x|, clamped at -126
+  const int emax = E ? (int)E - 126 : -126;  // frexp exponent of max|x|; subnormal maxima clamp to -126
   const int prec = min((int)maxprec, max(0, emax - minexp + 4));
   if (CODE) c[0] = c[1] = c[2] = 0ull;
   if (m == 0 || prec == 0) return 1u;  // one 0 bit
@@ -930,7 +882,7 @@ __device__ __forceinline__ uint32_t count_block1d_var(const float* f, int minexp
   const uint32_t m = max(max(a0, a1), max(a2, a3));
   special = m >= 0x7f800000u;
   const uint32_t E = special ? 150u : (m >> 23);
-  const int emax = (int)max(E, 1u) - 126;
+  const int emax = E ? (int)E - 126 : -126;
   const int prec = min((int)maxprec, max(0, emax - minexp + 4));
   if (m == 0 || prec == 0) return 1u;
   const int kmin = prec < 32 ? 32 - prec : 0;
@@ -1743,57 +1695,6 @@ template <> struct PipeWord<32> {
   static __device__ __forceinline__ uint64_t get(const T& v) { return (uint64_t)v; }
 };
 
-// Persistent fixed-rate 1-D decoder over full blocks [0, nfull) of a contiguous fp32 output, same hand-counted
-// pipeline as k_encode_fixed1d_pipe (one word load and one 16-B store per step).
-template <uint32_t WB, int NB>
-__global__ __launch_bounds__(256) void k_decode_fixed1d_pipe(const void* __restrict__ in, uint32_t nfull, Params p,
-                                                             float* __restrict__ out, uint64_t base_bits)
-{
-  __shared__ uint16_t dtab[5 * 8 * 128];
-  for (uint32_t t = threadIdx.x; t < 5 * 8 * 128 / 2; t += 256)  // 10 KiB, copied as dwords
-    ((uint32_t*)dtab)[t] = ((const uint32_t*)g_dec_tab1.v)[t];
-  __syncthreads();
-  constexpr uint32_t WBYTES = WB / 8;
-  // the caller guarantees base_bits % 32 == 0 (whole dwords: headerless streams and the 96-bit zfp header)
-  const pipe_v4i rin = buf_rsrc((const char*)in + base_bits / 8, nfull * WBYTES);
-  const __amdgpu_buffer_rsrc_t rout_b = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(nfull * 16u), 0x00020000);
-  const uint32_t stride = gridDim.x * 256u;
-  uint32_t b = blockIdx.x * 256u + threadIdx.x;
-  uint32_t bw = __builtin_amdgcn_readfirstlane(blockIdx.x * 256u + (threadIdx.x & ~63u));
-  if (bw >= nfull) return;
-  typename PipeWord<WB>::T r[NB];
-#pragma unroll
-  for (int d = 0; d < NB; d++) r[d] = PipeWord<WB>::load((b + d * stride) * WBYTES, rin);
-#pragma unroll
-  for (int d = 0; d < NB; d++) pipe_wait<0>(r[d]);
-  for (;;) {
-#pragma unroll
-    for (int k = 0; k < NB; k++) {
-      pipe_wait<2 * (NB - 1)>(r[k]);
-      float f[4];
-      bool special;
-      decode_block1d_fast<WB>(PipeWord<WB>::get(r[k]), dtab, f, special);
-      if (special && b < nfull) {
-        BitReader rd{(const uint64_t*)in, base_bits + (uint64_t)b * WB};
-        decode_block<1>(rd, p, f);
-      }
-      pipe_v4u v;
-      v.x = __float_as_uint(f[0]); v.y = __float_as_uint(f[1]); v.z = __float_as_uint(f[2]); v.w = __float_as_uint(f[3]);
-      // 16-B store through the compiler (it inserts the VALU-write -> wide-store wait states that an inline-asm
-      // store would need by hand; with an asm store lanes 12-15 of each row stored stale data). It still counts in
-      // vmcnt exactly once per step, as the hand-counted waits assume; aux 2 = non-temporal.
-      __builtin_amdgcn_raw_buffer_store_b128(v, rout_b, (int)(b * 16u), 0, 2);
-      r[k] = PipeWord<WB>::load((b + NB * stride) * WBYTES, rin);
-      b += stride;
-      bw += stride;
-      if (bw >= nfull) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        return;
-      }
-    }
-  }
-}
-
 // One-shot fixed-rate 1-D decoder (the shape of k_encode_fixed1d_np): each lane decodes U blocks 256 apart inside
 // its workgroup's chunk; the U word loads are issued before the table fill, and block k waits for its own word only
 // (U loads then k stores outstanding: vmcnt(U - 1)).
@@ -1825,7 +1726,10 @@ __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restric
     }
     pipe_v4u v;
     v.x = __float_as_uint(f[0]); v.y = __float_as_uint(f[1]); v.z = __float_as_uint(f[2]); v.w = __float_as_uint(f[3]);
-    __builtin_amdgcn_raw_buffer_store_b128(v, rout_b, (int)(b * 16u), 0, 2);  // see k_decode_fixed1d_pipe
+    // 16-B store through the compiler (it inserts the VALU-write -> wide-store wait states that an inline-asm store
+    // would need by hand; with an asm store lanes 12-15 of each row stored stale data). It still counts in vmcnt
+    // exactly once per block, as the hand-counted waits assume; aux 2 = non-temporal.
+    __builtin_amdgcn_raw_buffer_store_b128(v, rout_b, (int)(b * 16u), 0, 2);
   }
 }
 
@@ -2088,6 +1992,149 @@ __global__ void k_stitch(uint64_t* __restrict__ dst, uint64_t off, const uint64_
   dst[w] |= v;
 }
 
+// All shard streams in one launch (the receive side of a variable-rate all-gather): shard r
+// holds lens[r] bits at src + r * shard_words and lands at bit O_r = lens[0] + ... + lens[r - 1] (a per-lane running
+// sum over the shards: nshards is the world size). One lane per destination word, which it writes whole -- the OR of
+// every shard's bits that fall on it, zero past the stream's end -- so dst needs no zeroing and no atomics.
+__global__ __launch_bounds__(256) void k_stitch_shards(uint64_t* __restrict__ dst, uint64_t dst_words,
+                                                       const uint64_t* __restrict__ src, uint64_t shard_words,
+                                                       const uint64_t* __restrict__ lens, uint32_t nshards)
+{
+  const uint64_t w = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (w >= dst_words) return;
+  const uint64_t lo = w << 6;
+  uint64_t v = 0, off = 0;
+  for (uint32_t r = 0; r < nshards; r++) {
+    const uint64_t bits = lens[r];
+    const uint64_t end = off + bits;
+    if (bits && off < lo + 64 && end > lo) {
+      const uint64_t* sr = src + (uint64_t)r * shard_words;
+      const uint64_t nsw = (bits + 63) >> 6;
+      const int64_t sb = (int64_t)lo - (int64_t)off;  // shard bit landing on bit 0 of dst[w]
+      uint64_t x;
+      if (sb < 0) {
+        x = sr[0] << (uint32_t)(-sb);  // -sb < 64: the shard starts inside this word
+      } else {
+        const uint64_t i = (uint64_t)sb >> 6;  // < nsw: sb < bits
+        const uint32_t sh = (uint32_t)(sb & 63);
+        x = sr[i] >> sh;
+        if (sh && i + 1 < nsw) x |= sr[i + 1] << (64 - sh);
+      }
+      if (end < lo + 64) x &= (1ull << (end - lo)) - 1ull;  // drop the shard's own flush padding
+      v |= x;
+    }
+    off = end;
+  }
+  dst[w] = v;
+}
+
+// ------------------------------------------------------------------------------------------------ decode + mean
+// The receive side of the compressed all-gather hook: nstreams 1-D streams of the same shape
+// (one per rank, stream_words apart) are decoded and averaged in one launch instead of one decode and one add per
+// rank. Each lane accumulates in fp32 in rank order, acc = ((0 + x_0) + x_1) + ..., then stores acc / nstreams: the
+// values a sequence of decode -> add kernels would give (no contraction of the dequantising multiply into the add).
+
+// Fixed rate. WB = 64 / 32: the one-shot table decoder (whole-word blocks, kmin = 0); WB = 0: the generic decoder
+// (any fixed rate). One block per lane.
+template <uint32_t WB>
+__global__ __launch_bounds__(256) void k_decode_mean_fixed1d(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                             uint64_t stream_words, uint32_t nstreams)
+{
+#pragma clang fp contract(off)
+  __shared__ uint16_t dtab[WB ? 5 * 8 * 128 : 1];
+  if (WB) {
+    for (uint32_t t = threadIdx.x; t < 5 * 8 * 128 / 2; t += 256) ((uint32_t*)dtab)[t] = ((const uint32_t*)g_dec_tab1.v)[t];
+    __syncthreads();
+  }
+  const uint64_t b = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (b >= F.nblocks) return;
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (uint32_t r = 0; r < nstreams; r++) {
+    const uint64_t* sr = in + (uint64_t)r * stream_words;
+    float f[4];
+    bool special = true;
+    if constexpr (WB == 64) decode_block1d_fast<64>(sr[b], dtab, f, special);
+    else if constexpr (WB == 32) decode_block1d_fast<32>(((const uint32_t*)sr)[b], dtab, f, special);
+    if (special) {
+      BitReader rd{sr, b * p.maxbits};
+      decode_block<1>(rd, p, f);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) acc[i] = acc[i] + f[i];
+  }
+  const float nf = (float)nstreams;
+#pragma unroll
+  for (int i = 0; i < 4; i++) acc[i] = acc[i] / nf;
+  scatter_block<1>(F, (uint32_t)b, acc);
+}
+
+// Variable rate (1-D closed-form domain) with each stream's block index every 16 blocks (index_words entries apart):
+// the shape of k_decode1d_var_staged -- LANES chunks of 16 blocks per workgroup, the workgroup's span of each stream
+// staged in LDS in turn -- with the 16 blocks' 64 values accumulated in registers across the streams and stored once.
+template <uint32_t LANES>
+__global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                             uint64_t stream_words, const uint64_t* __restrict__ index,
+                                                             uint64_t index_words, uint64_t nchunks, uint32_t nstreams)
+{
+#pragma clang fp contract(off)
+  constexpr uint32_t CAP = LANES * 16 * 80 / 64;
+  __shared__ uint16_t dt7[5 * 128];
+  __shared__ uint64_t sw[CAP + 2];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t t = tid; t < 5 * 128; t += LANES) dt7[t] = g_dec_tab1.v[(((t >> 7) << 3) | 7u) << 7 | (t & 127u)];
+  const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
+  const uint64_t c = c0 + tid;
+  const uint64_t b0 = c * 16, b1 = min<uint64_t>(b0 + 16, F.nblocks);
+  float acc[16][4];
+#pragma unroll
+  for (int k = 0; k < 16; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
+  for (uint32_t r = 0; r < nstreams; r++) {
+    const uint64_t* sr = in + (uint64_t)r * stream_words;
+    const uint64_t* ix = index + (uint64_t)r * index_words;
+    const uint64_t w0 = ix[c0] >> 6;
+    const uint64_t wend = c0 + LANES < nchunks ? ((ix[c0 + LANES] + 63) >> 6) : stream_words;
+    const uint64_t span = min<uint64_t>(wend, stream_words) - w0;
+    const bool staged = span <= CAP;
+    __syncthreads();  // the previous stream's span is no longer read
+    if (staged)
+      for (uint32_t j = tid; j < (uint32_t)span + 2; j += LANES) sw[j] = w0 + j < stream_words ? sr[w0 + j] : 0ull;
+    __syncthreads();
+    if (c >= nchunks) continue;
+    uint64_t pos = ix[c];
+    auto run = [&](const auto& win) {
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        if (b0 + k < b1) {
+          float f[4];
+          decode_block1d_var(win, pos, dt7, p.minexp, p.maxprec, f);
+#pragma unroll
+          for (int i = 0; i < 4; i++) acc[k][i] = acc[k][i] + f[i];
+        }
+      }
+    };
+    if (staged) {
+      pos -= 64 * w0;
+      run(LdsWindow{sw});
+    } else {
+      run(GlobalWindow{sr});
+    }
+  }
+  if (c >= nchunks) return;
+  const float nf = (float)nstreams;
+  float* out = (float*)F.data;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint64_t b = b0 + k;
+    if (b < b1) {
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) v[i] = acc[k][i] / nf;
+      if (F.vec && 4 * b + 4 <= F.n[0]) *(float4*)(out + 4 * b) = make_float4(v[0], v[1], v[2], v[3]);
+      else scatter_block<1>(F, (uint32_t)b, v);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ stages
 template <int D>
 __global__ void k_stage_emax(const float* __restrict__ blocks, uint32_t n, int32_t* __restrict__ emax)
@@ -2220,59 +2267,24 @@ __global__ void k_fill_normal(float* __restrict__ out, uint64_t count, double si
 // ------------------------------------------------------------------------------------------------ launchers
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
-static int g_fixed1d_variant = -1;
-
-static int fixed1d_variant()
-{
-  if (g_fixed1d_variant < 0) {
-    const char* e = getenv("GCOW_FIXED1D_VARIANT");
-    g_fixed1d_variant = e ? atoi(e) : 8;  // 8/12/16 = one-shot lean-5 with U blocks per lane; 5 = persistent
-                                             // grid-stride lean-5, 1 = generic coder (A/B, parity bisection)
-  }
-  return g_fixed1d_variant;
-}
-
-static int decode1d_variant()
-{
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("GCOW_DECODE1D_VARIANT");
-    v = e ? atoi(e) : 16;  // 8 / 16 = one-shot with U blocks per lane, 0 = persistent pipeline
-  }
-  return v;
-}
-
-static int fixed1d_wgs_per_cu(int dflt = 32)
-{
-  const char* e = getenv("GCOW_FIXED1D_WGS");
-  return e ? atoi(e) : dflt;
-}
-
 template <int DT, uint32_t WB>
 static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, void* out, hipStream_t st)
 {
   const uint32_t nfull = (uint32_t)(nvals / 4);
-  const uint32_t grid = (nfull + 511) / 512;
-  if (grid) {
+  if (nfull) {
     // the lean coder needs prec >= 32 for every nonzero block: e >= -126 => e - minexp + 4 >= 32
     const bool kmin0 = p.maxprec >= 32 && p.minexp <= -154;
-    if (!kmin0 || fixed1d_variant() == 1) {
-      k_encode_fixed1d_generic<DT, WB><<<grid, 256, 0, st>>>(in, nfull, p, out);
+    if (!kmin0) {
+      k_encode_fixed1d_generic<DT, WB><<<(nfull + 511) / 512, 256, 0, st>>>(in, nfull, p, out);
     } else {
-      // chunks keep every buffer offset (block + NB * stride) * 16 below 2^32
+      // one-shot grid, U = 8 blocks per lane; chunks keep every buffer offset below 2^32
       constexpr uint32_t CH = 1u << 27;
       constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;
-      const uint32_t wgs = (uint32_t)fixed1d_wgs_per_cu(12);
-      const int var = fixed1d_variant();
       for (uint32_t c0 = 0; c0 < nfull; c0 += CH) {
         const uint32_t nc = min(CH, nfull - c0);
-        const uint32_t g = min((nc + 255) / 256, 256u * wgs);
         const void* ic = (const char*)in + (size_t)c0 * IB;
         void* oc = (char*)out + (size_t)c0 * (WB / 8);
-        if (var == 16) k_encode_fixed1d_np<DT, WB, 16><<<(nc + 4095) / 4096, 256, 0, st>>>(ic, nc, p, oc);
-        else if (var == 8) k_encode_fixed1d_np<DT, WB, 8><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
-        else if (var == 12) k_encode_fixed1d_np<DT, WB, 12><<<(nc + 3071) / 3072, 256, 0, st>>>(ic, nc, p, oc);
-        else k_encode_fixed1d_pipe<DT, WB, 3><<<g, 256, 0, st>>>(ic, nc, p, oc);
+        k_encode_fixed1d_np<DT, WB, 8><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
       }
     }
   }
@@ -2306,7 +2318,7 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
     kern<<<plan.nranges, T, lds, st>>>(F, p, plan.range, nullptr, out32, index, index_shift);
     return hipGetLastError();
   }
-  const bool var1d = D == 1 && T == 256 && p.minbits <= 1 && p.maxbits >= 160 && !getenv("GCOW_GENERIC_VAR");
+  const bool var1d = D == 1 && T == 256 && p.minbits <= 1 && p.maxbits >= 160;
   if (var1d) k_count1d_var<DT, 4><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   else k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   k_scan_ranges<<<1, 1024, 0, st>>>(ws_sums, plan.nranges, ws_base, d_total, out32, d_base);
@@ -2344,7 +2356,7 @@ hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in
                          uint32_t chunk, uint64_t nchunks, bool fixed, uint64_t base_bits, uint64_t* end_out,
                          void* stream, uint64_t in_words)
 {
-  if (chunk == 1 && in_words && (fixed || index) && F.dims >= 2 && !getenv("GCOW_DECODE_GLOBAL")) {
+  if (chunk == 1 && in_words && (fixed || index) && F.dims >= 2) {
     const uint32_t g = (uint32_t)((F.nblocks + 63) / 64);
     if (F.dims == 2) k_decode_staged<2><<<g, 64, 0, S(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
     else k_decode_staged<3><<<g, 64, 0, S(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
@@ -2382,8 +2394,7 @@ static hipError_t launch_dec3d_t(const FieldDesc& F, const Params& p, const uint
 bool fixed3d_ok(uint32_t maxbits)
 {
   const uint32_t w = maxbits / 32;
-  return maxbits % 32 == 0 && (w == 2 || w == 4 || w == 8 || w == 16 || w == 32 || w == 64) &&
-         !getenv("GCOW_GENERIC_3D");
+  return maxbits % 32 == 0 && (w == 2 || w == 4 || w == 8 || w == 16 || w == 32 || w == 64);
 }
 
 hipError_t launch_encode3d_fixed(const FieldDesc& F, const Params& p, uint32_t* out32, void* stream)
@@ -2453,14 +2464,9 @@ hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64
                                const uint64_t* index, uint32_t chunk, uint64_t nchunks, uint64_t base_bits,
                                uint64_t* end_out, void* stream)
 {
-  const char* vm = getenv("GCOW_VDEC");  // "global" / "staged256" (A/B); default staged, 128 lanes
-  if (index && chunk == 16 && in_words && !(vm && !strcmp(vm, "global"))) {
-    if (!(vm && !strcmp(vm, "staged256")))
-      k_decode1d_var_staged<128><<<(uint32_t)((nchunks + 127) / 128), 128, 0, S(stream)>>>(F, p, in, in_words, index,
-                                                                                            nchunks, base_bits, end_out);
-    else
-      k_decode1d_var_staged<256><<<(uint32_t)((nchunks + 255) / 256), 256, 0, S(stream)>>>(F, p, in, in_words, index,
-                                                                                            nchunks, base_bits, end_out);
+  if (index && chunk == 16 && in_words) {  // the workgroup's stream span staged in LDS, 128 lanes
+    k_decode1d_var_staged<128><<<(uint32_t)((nchunks + 127) / 128), 128, 0, S(stream)>>>(F, p, in, in_words, index,
+                                                                                          nchunks, base_bits, end_out);
     return hipGetLastError();
   }
   k_decode1d_var<<<(uint32_t)((nchunks + 255) / 256), 256, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, base_bits,
@@ -2473,23 +2479,12 @@ hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint
 {
   const uint32_t nfull = (uint32_t)(F.n[0] / 4);
   constexpr uint32_t CH = 1u << 27;
-  const uint32_t wgs = (uint32_t)fixed1d_wgs_per_cu(12);
-  for (uint32_t c0 = 0; c0 < nfull; c0 += CH) {
+  for (uint32_t c0 = 0; c0 < nfull; c0 += CH) {  // one-shot grid, U = 16 words per lane
     const uint32_t nc = min(CH, nfull - c0);
-    const uint32_t g = min((nc + 255) / 256, 256u * wgs);
     float* out = (float*)F.data + (size_t)c0 * 4;
     const uint64_t bb = base_bits + (uint64_t)c0 * p.maxbits;
-    const int var = decode1d_variant();
-    if (var == 0) {  // persistent grid-stride pipeline (A/B)
-      if (p.maxbits == 64) k_decode_fixed1d_pipe<64, 3><<<g, 256, 0, S(stream)>>>(in, nc, p, out, bb);
-      else k_decode_fixed1d_pipe<32, 3><<<g, 256, 0, S(stream)>>>(in, nc, p, out, bb);
-    } else if (var == 8) {
-      if (p.maxbits == 64) k_decode_fixed1d_np<64, 8><<<(nc + 2047) / 2048, 256, 0, S(stream)>>>(in, nc, p, out, bb);
-      else k_decode_fixed1d_np<32, 8><<<(nc + 2047) / 2048, 256, 0, S(stream)>>>(in, nc, p, out, bb);
-    } else {
-      if (p.maxbits == 64) k_decode_fixed1d_np<64, 16><<<(nc + 4095) / 4096, 256, 0, S(stream)>>>(in, nc, p, out, bb);
-      else k_decode_fixed1d_np<32, 16><<<(nc + 4095) / 4096, 256, 0, S(stream)>>>(in, nc, p, out, bb);
-    }
+    if (p.maxbits == 64) k_decode_fixed1d_np<64, 16><<<(nc + 4095) / 4096, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+    else k_decode_fixed1d_np<32, 16><<<(nc + 4095) / 4096, 256, 0, S(stream)>>>(in, nc, p, out, bb);
   }
   if (F.n[0] % 4) k_decode_tail1d<<<1, 1, 0, S(stream)>>>(F, p, in, base_bits, nfull);
   return hipGetLastError();
@@ -2516,6 +2511,34 @@ hipError_t launch_stitch(uint64_t* dst, uint64_t off, const uint64_t* src, uint6
   const uint64_t words = ((off + bits + 63) >> 6) - (off >> 6);
   const uint64_t grid = (words + 255) / 256;
   k_stitch<<<grid, 256, 0, S(stream)>>>(dst, off, src, bits);
+  return hipGetLastError();
+}
+
+hipError_t launch_stitch_shards(uint64_t* dst, uint64_t dst_words, const uint64_t* src, uint64_t shard_words,
+                                const uint64_t* lens, uint32_t nshards, void* stream)
+{
+  const uint64_t grid = (dst_words + 255) / 256;
+  if (!grid) return hipSuccess;
+  k_stitch_shards<<<(uint32_t)grid, 256, 0, S(stream)>>>(dst, dst_words, src, shard_words, lens, nshards);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t stream_words,
+                                uint32_t nstreams, const uint64_t* index, uint64_t index_words, void* stream)
+{
+  if (!F.nblocks) return hipSuccess;
+  hipStream_t st = S(stream);
+  if (p.minbits == p.maxbits) {
+    const uint32_t g = (F.nblocks + 255) / 256;
+    const bool lean = p.maxprec >= 32 && p.minexp <= -154;
+    if (lean && p.maxbits == 64) k_decode_mean_fixed1d<64><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams);
+    else if (lean && p.maxbits == 32) k_decode_mean_fixed1d<32><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams);
+    else k_decode_mean_fixed1d<0><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams);
+    return hipGetLastError();
+  }
+  const uint64_t nchunks = (F.nblocks + 15) / 16;
+  k_decode_mean1d_var<128><<<(uint32_t)((nchunks + 127) / 128), 128, 0, st>>>(F, p, in, stream_words, index,
+                                                                               index_words, nchunks, nstreams);
   return hipGetLastError();
 }
 

@@ -8,32 +8,33 @@ PCIe copies per step. Two device-resident replacements:
 * `roundtrip_hook` -- the reference's exact semantics (mean all-reduce, then encode -> decode of the reduced
   bucket), on the GPU: no `.cpu()`, no `torch.from_numpy(...).to(device)`.
 * `compressed_allgather_hook` -- gradients compressed *before* the wire: each rank encodes its bucket, the
-  compressed streams are all-gathered over RCCL, every rank decodes all of them and averages. At rate r the wire
-  carries r/32 of the fp32 bytes per rank.
+  compressed streams are all-gathered over RCCL, and one launch decodes every rank's stream and averages them
+  (gcow_decode_mean_device: acc = 0 + x_0 + x_1 + ... in rank order, then / world). At rate r the wire carries r/32
+  of the fp32 bytes per rank.
 
-Both register with `ddp_model.register_comm_hook(GcowHookState(...), hook)`.
+Both register with `ddp_model.register_comm_hook(GcowHookState(...), hook)`. `GcowHookState.codec` defaults to the
+device codec (gcow_amd.dist.DeviceCodec); tests inject an oracle-backed codec to run the hook bodies over gloo.
 """
 from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
 
-from . import codec
+from . import codec as _codec
+from . import dist as gdist
 from ._ffi import GcowParams
+
+INDEX_STRIDE = 16  # block index spacing the multi-stream decoder reads (one entry per 16 blocks)
 
 
 @dataclass
 class GcowHookState:
-    params: GcowParams = field(default_factory=lambda: codec.rate(16, 1))
+    params: GcowParams = field(default_factory=lambda: _codec.rate(16, 1))
     process_group: object = None
-    index_stride: int = 16  # variable-rate streams carry a block index for parallel decode
-    encoders: dict = field(default_factory=dict)
+    codec: object = None  # None: gcow_amd.dist.device_codec()
 
-    def encoder(self, n: int, dtype, device, index_stride=0):
-        key = (n, dtype, device, index_stride)
-        if key not in self.encoders:
-            self.encoders[key] = codec.Encoder((n,), dtype, self.params, device, index_stride)
-        return self.encoders[key]
+    def get_codec(self):
+        return self.codec or gdist.device_codec()
 
 
 def _done(t: torch.Tensor) -> torch.futures.Future[torch.Tensor]:
@@ -42,20 +43,25 @@ def _done(t: torch.Tensor) -> torch.futures.Future[torch.Tensor]:
     return fut
 
 
+def _flat(buf: torch.Tensor):
+    flat = buf.reshape(-1)
+    return flat, (flat if flat.dtype in (torch.float32, torch.bfloat16) else flat.float())
+
+
 def roundtrip_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.Tensor]:
     """Mean all-reduce, then the lossy encode -> decode the reference applies (zfpy), device-resident."""
     group = state.process_group
     buf = bucket.buffer()
     world = dist.get_world_size(group)
     fut = dist.all_reduce(buf.div_(world), group=group, async_op=True).get_future()
+    cdc = state.get_codec()
 
     def lossy(f):
         t = f.value()[0]
-        flat = t.reshape(-1)
-        x = flat if flat.dtype in (torch.float32, torch.bfloat16) else flat.float()
-        stride = 0 if codec.is_fixed(state.params) else state.index_stride
-        e = state.encoder(x.numel(), x.dtype, x.device, stride)(x)
-        out = codec.decode(e)
+        flat, x = _flat(t)
+        stride = 0 if _codec.is_fixed(state.params) else INDEX_STRIDE
+        words, _, index = cdc.encode(x, state.params, stride)
+        out = cdc.decode(words, x.numel(), state.params, index=index, index_stride=stride)
         flat.copy_(out.to(flat.dtype))
         return t
 
@@ -63,47 +69,28 @@ def roundtrip_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.T
 
 
 def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.Tensor]:
-    """Encode locally, all-gather compressed streams, decode every rank's stream and average."""
+    """Encode locally, all-gather the compressed streams, decode every rank's stream and average (one launch)."""
     group = state.process_group
     buf = bucket.buffer()
     world = dist.get_world_size(group)
-    flat = buf.reshape(-1)
-    x = flat if flat.dtype in (torch.float32, torch.bfloat16) else flat.float()
+    flat, x = _flat(buf)
     n = x.numel()
     p = state.params
-    if codec.is_fixed(p):
-        e = state.encoder(n, x.dtype, x.device)(x)
-        nb = (n + 3) // 4
-        nw = (nb * p.maxbits + 63) // 64
-        local = e.words[:nw].contiguous()
-        gathered = torch.empty(world * nw, dtype=torch.int64, device=x.device)
-        dist.all_gather_into_tensor(gathered, local, group=group)
-        acc = torch.zeros(n, dtype=torch.float32, device=x.device)
-        tmp = torch.empty(n, dtype=torch.float32, device=x.device)
-        for r in range(world):
-            words = torch.cat([gathered[r * nw:(r + 1) * nw], torch.zeros(2, dtype=torch.int64, device=x.device)])
-            codec.decode(words, (n,), p, out=tmp)
-            acc += tmp
+    cdc = state.get_codec()
+    if _codec.is_fixed(p):
+        words, _, _ = cdc.encode(x, p)
+        nw = ((n + 3) // 4 * p.maxbits + 63) // 64
+        gathered = gdist.allgather_padded(words, nw, nw, group, pad=2)
+        mean = cdc.decode_mean(gathered, nw, world, n, p)
     else:
-        stride = state.index_stride
-        e = state.encoder(n, x.dtype, x.device, stride)(x)
-        lens = torch.empty(world, dtype=torch.int64, device=x.device)
-        dist.all_gather_into_tensor(lens, e.bits_dev.reshape(1), group=group)
-        lens_h = lens.cpu().tolist()
-        maxw = max(1, max((b + 63) // 64 for b in lens_h)) + 2
-        local = torch.zeros(maxw, dtype=torch.int64, device=x.device)
-        nw = (lens_h[dist.get_rank(group)] + 63) // 64
-        local[:nw] = e.words[:nw]
-        gathered = torch.empty(world * maxw, dtype=torch.int64, device=x.device)
-        dist.all_gather_into_tensor(gathered, local, group=group)
-        ni = e.index.numel()
+        words, bits, index = cdc.encode(x, p, INDEX_STRIDE)
+        lens, lens_h = gdist.gather_lengths(bits, x.device, group)
+        maxw = max(1, max((b + 63) // 64 for b in lens_h))
+        rank = dist.get_rank(group)
+        gathered = gdist.allgather_padded(words, (lens_h[rank] + 63) // 64, maxw, group, pad=2)
+        ni = index.numel()
         idx = torch.empty(world * ni, dtype=torch.int64, device=x.device)
-        dist.all_gather_into_tensor(idx, e.index, group=group)
-        acc = torch.zeros(n, dtype=torch.float32, device=x.device)
-        tmp = torch.empty(n, dtype=torch.float32, device=x.device)
-        for r in range(world):
-            codec.decode(gathered[r * maxw:(r + 1) * maxw], (n,), p, index=idx[r * ni:(r + 1) * ni],
-                         index_stride=stride, out=tmp)
-            acc += tmp
-    flat.copy_((acc / world).to(flat.dtype))
+        gdist.allgather_into(idx, index[:ni].contiguous(), group)
+        mean = cdc.decode_mean(gathered, maxw, world, n, p, idx, ni, INDEX_STRIDE)
+    flat.copy_(mean.to(flat.dtype))
     return _done(buf)

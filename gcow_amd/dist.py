@@ -7,12 +7,13 @@ hw/models/train_imagenet.py:446-475); this is the exchange step north_star asks 
 Fixed rate: every block is maxbits long, so shard r's stream occupies bits [r*S*maxbits, ...) of the full stream;
 with S*maxbits a multiple of 64 one all-gather of equal-size shard streams IS the single-GPU stream (byte-identical
 to encoding the whole bucket on one GPU).
-Variable rate: all-gather the per-rank bit lengths, all-gather the streams padded to the longest, then bit-stitch
-shard r at its exclusive-prefix bit offset (gcow_stitch_device on the GPU). Per-shard flush padding is dropped:
-offsets use the unflushed bit counts.
+Variable rate: all-gather the per-rank bit lengths (device tensors), all-gather the streams padded to the longest,
+then one launch stitches every shard at its exclusive-prefix bit offset (gcow_stitch_shards_device: the prefix is
+taken on the device from the gathered lengths). Per-shard flush padding is dropped: offsets use the unflushed bit
+counts. The host reads the gathered lengths once, to size the padded buffers.
 
-The protocol functions take plain int64 word tensors, so the same code runs over RCCL on device tensors and over
-gloo on CPU tensors (tests/test_dist_cpu.py).
+The codec work is injectable: every function takes `codec=` (default `DeviceCodec`, the gfx950 kernels), so the
+protocol code itself runs unchanged over gloo on CPU tensors with an oracle-backed codec in tests/test_dist_cpu.py.
 """
 from __future__ import annotations
 
@@ -22,9 +23,52 @@ import torch.distributed as dist
 from ._ffi import GcowError
 
 
+class DeviceCodec:
+    """The codec calls the exchange needs, on device tensors through libgcow.so. Encoders are cached per
+    (shape, dtype, params, index stride) so a repeated bucket allocates nothing."""
+
+    def __init__(self):
+        self._enc = {}
+
+    def encode(self, x: torch.Tensor, params, index_stride: int = 0):
+        """-> (words int64 tensor, bits int64[1] tensor on x.device, block index or None)."""
+        from . import codec
+        x = x.reshape(-1)
+        key = (x.numel(), x.dtype, x.device, params.tuple(), index_stride)
+        enc = self._enc.get(key)
+        if enc is None:
+            enc = self._enc[key] = codec.Encoder((x.numel(),), x.dtype, params, x.device, index_stride)
+        e = enc(x if x.is_contiguous() else x.contiguous())
+        return e.words, e.bits_dev, e.index
+
+    def stitch_shards(self, dst, src, shard_words: int, lens, nshards: int):
+        from . import codec
+        return codec.stitch_shards(dst, src, shard_words, lens[:nshards])
+
+    def decode(self, words, n: int, params, index=None, index_stride: int = 0, out=None):
+        from . import codec
+        return codec.decode(words, (n,), params, index=index, index_stride=index_stride, out=out)
+
+    def decode_mean(self, streams, stream_words: int, nstreams: int, n: int, params, index=None,
+                    index_words: int = 0, index_stride: int = 0, out=None):
+        from . import codec
+        return codec.decode_mean(streams, stream_words, nstreams, n, params, index, index_words, index_stride, out)
+
+
+_DEVICE = None
+
+
+def device_codec() -> DeviceCodec:
+    global _DEVICE
+    if _DEVICE is None:
+        _DEVICE = DeviceCodec()
+    return _DEVICE
+
+
 def shard_bounds(nvals: int, world: int, rank: int, block: int = 4, align_blocks: int = 16):
     """Contiguous block-aligned shard [lo, hi) of a 1-D bucket of nvals values for `rank`. align_blocks = 16 makes
-    every full shard end on a 64-bit stream boundary at any rate with 4 * rate integral."""
+    every full shard end on a 64-bit stream boundary at any rate with 4 * rate integral. Small buckets leave the last
+    ranks an empty shard (lo == hi == nvals); they still take part in every collective."""
     nblocks = (nvals + block - 1) // block
     per = (nblocks + world - 1) // world
     per = (per + align_blocks - 1) // align_blocks * align_blocks
@@ -33,12 +77,19 @@ def shard_bounds(nvals: int, world: int, rank: int, block: int = 4, align_blocks
     return min(lo_b * block, nvals), min(hi_b * block, nvals)
 
 
-def _allgather_into(out: torch.Tensor, local: torch.Tensor, group=None):
-    if dist.get_backend(group) == "nccl":
+def is_nccl(group=None) -> bool:
+    return dist.get_backend(group) == "nccl"
+
+
+def allgather_into(out: torch.Tensor, local: torch.Tensor, group=None):
+    """out = concat over ranks of `local` (equal sizes): one all_gather_into_tensor on RCCL, a list all_gather on
+    gloo."""
+    if is_nccl(group):
         dist.all_gather_into_tensor(out, local, group=group)
     else:
         world = dist.get_world_size(group)
         dist.all_gather(list(out.chunk(world)), local, group=group)
+    return out
 
 
 def allgather_fixed(words: torch.Tensor, nblocks: int, maxbits: int, group=None) -> torch.Tensor:
@@ -49,49 +100,63 @@ def allgather_fixed(words: torch.Tensor, nblocks: int, maxbits: int, group=None)
     local = words[:nw].contiguous()
     world = dist.get_world_size(group)
     out = torch.empty(world * nw, dtype=torch.int64, device=local.device)
-    _allgather_into(out, local, group)
+    allgather_into(out, local, group)
     return out
 
 
-def allgather_variable(words: torch.Tensor, bits: int, group=None, stitch=None):
-    """All-gather variable-rate shard streams and stitch them into one stream. Returns (words, total_bits).
-    `stitch(dst, dst_bit_offset, src, src_bits)` defaults to the device kernel (gcow_stitch_device)."""
-    if stitch is None:
-        from .codec import stitch as _dev_stitch
-        stitch = _dev_stitch
+def gather_lengths(bits, device, group=None):
+    """All-gather one unflushed bit count per rank (an int or an int64[1] tensor): -> (device tensor, host list)."""
     world = dist.get_world_size(group)
-    dev = words.device
-    lens = torch.zeros(world, dtype=torch.int64, device=dev)
-    mine = torch.tensor([int(bits)], dtype=torch.int64, device=dev)
-    _allgather_into(lens, mine, group)
-    lens_h = [int(v) for v in lens.cpu().tolist()]
+    mine = bits.reshape(1).to(device=device, dtype=torch.int64) if isinstance(bits, torch.Tensor) else \
+        torch.tensor([int(bits)], dtype=torch.int64, device=device)
+    lens = torch.empty(world, dtype=torch.int64, device=device)
+    allgather_into(lens, mine, group)
+    return lens, [int(v) for v in lens.tolist()]  # the one host read: it sizes the padded buffers
+
+
+def allgather_padded(words: torch.Tensor, nw: int, maxw: int, group=None, pad: int = 0) -> torch.Tensor:
+    """All-gather each rank's first nw words padded with zeros to maxw: -> world * maxw (+ pad zero) words."""
+    world = dist.get_world_size(group)
+    local = torch.zeros(maxw, dtype=torch.int64, device=words.device)
+    if nw:
+        local[:nw] = words[:nw]
+    out = torch.zeros(world * maxw + pad, dtype=torch.int64, device=words.device)
+    allgather_into(out[: world * maxw], local, group)
+    return out
+
+
+def allgather_variable(words: torch.Tensor, bits, group=None, codec=None):
+    """All-gather variable-rate shard streams and stitch them into one stream. `bits`: this rank's unflushed bit
+    count (int or int64[1] tensor on words' device). Returns (words, total_bits)."""
+    codec = codec or device_codec()
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    lens, lens_h = gather_lengths(bits, words.device, group)
     maxw = max(1, max((b + 63) // 64 for b in lens_h))
-    local = torch.zeros(maxw, dtype=torch.int64, device=dev)
-    nw = (int(bits) + 63) // 64
-    local[:nw] = words[:nw]
-    gathered = torch.empty(world * maxw, dtype=torch.int64, device=dev)
-    _allgather_into(gathered, local, group)
+    gathered = allgather_padded(words, (lens_h[rank] + 63) // 64, maxw, group)
     total = sum(lens_h)
-    out = torch.zeros((total + 63) // 64 + 1, dtype=torch.int64, device=dev)
-    off = 0
-    for r in range(world):
-        if lens_h[r]:
-            stitch(out, off, gathered[r * maxw:(r + 1) * maxw], lens_h[r])
-        off += lens_h[r]
+    out = torch.empty(max((total + 63) // 64, 1), dtype=torch.int64, device=words.device)
+    codec.stitch_shards(out, gathered, maxw, lens, world)
     return out[: (total + 63) // 64], total
 
 
-def encode_allgather(bucket: torch.Tensor, params, group=None):
+def encode_allgather(bucket: torch.Tensor, params, group=None, codec=None):
     """Encode this rank's contiguous shard of a 1-D bucket (replicated on every rank: the C4 layout) and rebuild the
-    full stream on every rank. Returns (words, total_bits)."""
-    from . import codec
+    full stream on every rank. Returns (words, total_bits). A rank whose shard is empty (small buckets) joins the
+    exchange with zero bits instead of encoding."""
+    codec = codec or device_codec()
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     bounds = [shard_bounds(bucket.numel(), world, r) for r in range(world)]
     lo, hi = bounds[rank]
-    enc = codec.encode(bucket[lo:hi], params)
+    fixed = params.minbits == params.maxbits
+    if hi > lo:
+        words, bits, _ = codec.encode(bucket[lo:hi], params)
+    else:
+        words, bits = torch.zeros(1, dtype=torch.int64, device=bucket.device), 0
     sizes = {b - a for a, b in bounds}
     nb = (hi - lo + 3) // 4
-    if codec.is_fixed(params) and len(sizes) == 1 and (hi - lo) % 4 == 0 and (nb * params.maxbits) % 64 == 0:
-        words = allgather_fixed(enc.words, nb, params.maxbits, group)
-        return words, world * nb * params.maxbits
-    return allgather_variable(enc.words, enc.bits, group)
+    if fixed and len(sizes) == 1 and (hi - lo) % 4 == 0 and (nb * params.maxbits) % 64 == 0:
+        out = allgather_fixed(words, nb, params.maxbits, group)
+        return out, world * nb * params.maxbits
+    if fixed:  # ragged shards: the bit counts are known on the host
+        bits = nb * params.maxbits
+    return allgather_variable(words, bits, group, codec)

@@ -253,6 +253,28 @@ gcow_status gcow_stitch_device(uint64_t* d_dst, uint64_t dst_bit_offset, const u
                                void* hip_stream);
 
 /*
+ * The whole receive side of a sharded variable-rate all-gather in one launch: nshards shard
+ * streams of d_lens[r] bits (DEVICE uint64 array; the per-rank unflushed bit counts), stored shard_words apart from
+ * d_src (the padded all-gather buffer), are concatenated bit-exactly -- shard r at bit d_lens[0] + ... + d_lens[r-1],
+ * its flush padding dropped -- into d_dst, all of whose dst_words words are written (zero past the stream's end: the
+ * single stream's flush). Equal to one gcow_encode_device of the unsharded bucket. d_dst needs no zeroing.
+ */
+gcow_status gcow_stitch_shards_device(uint64_t* d_dst, uint64_t dst_words, const uint64_t* d_src, uint64_t shard_words,
+                                      const uint64_t* d_lens, uint32_t nshards, void* hip_stream);
+
+/*
+ * Decode-and-average of nstreams 1-D streams of one bucket shape (the compressed all-gather DDP hook's receive side;
+ * hw/models/train_imagenet.py:446-475 is the caller contract): field->data (DEVICE fp32, 1-D) receives, elementwise
+ * in fp32, ((0 + x_0) + x_1 + ... + x_{n-1}) / nstreams with x_r the libzfp decode of stream r. Streams start
+ * stream_words words apart at d_streams; the buffer must have 2 readable words past the last stream. Fixed rate: any
+ * parameters. Variable rate: minbits <= 1, maxbits >= 160 (accuracy / precision / expert) and every stream's block
+ * index (index_stride 16, entries index_words apart at d_index, as gcow_encode_device writes them).
+ */
+gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p, const uint64_t* d_streams,
+                                    uint64_t stream_words, uint32_t nstreams, const uint64_t* d_index,
+                                    uint64_t index_words, uint32_t index_stride, void* hip_stream);
+
+/*
  * zfp 0.5.5 stream header: the byte format zfpy.compress_numpy writes (hw/models/train_imagenet.py:459-465 calls
  * it), i.e. libzfp zfp_write_header(ZFP_HEADER_FULL): magic 'z','f','p' + codec version 5 (32 bits), field metadata
  * (52 bits: sizes, dims - 1, type - 1) and the compression mode (12-bit short form for rate / precision /

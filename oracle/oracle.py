@@ -40,7 +40,37 @@ def lib():
         path = os.path.join(HERE, "liboracle.so")
         if not os.path.exists(path):
             build()
-        L = C.CDLL(path)
+        _lib = _bind(C.CDLL(path))
+    return _lib
+
+
+_native = None
+
+
+def native_lib():
+    """The restatement compiled for the host it runs on (gcc -O3 -march=native, into a temp dir): the CPU-baseline
+    build. Returns (lib, flags); falls back to the prebuilt liboracle.so (-march=x86-64-v2)
+    when no compiler is available."""
+    global _native
+    if _native is None:
+        import shutil
+        import tempfile
+        flags = ["-O3", "-march=native"]
+        cc = shutil.which("gcc")
+        if cc:
+            d = tempfile.mkdtemp(prefix="gcow_oracle_native_")
+            so = os.path.join(d, "liboracle_native.so")
+            r = subprocess.run([cc, *flags, "-fPIC", "-shared", "-pthread", "-o", so, os.path.join(HERE, "zfp_oracle.c"),
+                                "-lm"], capture_output=True)
+            if r.returncode == 0:
+                _native = (_bind(C.CDLL(so)), " ".join(flags))
+        if _native is None:
+            _native = (lib(), "-O3 -march=x86-64-v2 (prebuilt; no compiler)")
+    return _native
+
+
+def _bind(L):
+    if True:
         P = C.POINTER
         L.orc_block_exponent.restype = C.c_int
         L.orc_block_exponent.argtypes = [P(C.c_float), C.c_uint]
@@ -88,8 +118,7 @@ def lib():
         L.orc_write_header.argtypes = [P(C.c_uint64), C.c_uint, P(C.c_size_t), C.c_uint, P(Params)]
         L.orc_read_header.restype = C.c_uint
         L.orc_read_header.argtypes = [P(C.c_uint64), P(C.c_uint), P(C.c_size_t), P(C.c_uint), P(Params)]
-        _lib = L
-    return _lib
+    return L
 
 
 def ref():
@@ -166,7 +195,7 @@ def max_words(shape, p: Params) -> int:
     return (nb * mb + 63) // 64 + 2
 
 
-def compress(arr: np.ndarray, p: Params, threads: int = 0):
+def compress(arr: np.ndarray, p: Params, threads: int = 0, L=None):
     """Encode a C-contiguous float32 (or bf16-as-uint16) array. Returns (words[uint64], total_bits)."""
     arr = np.ascontiguousarray(arr)
     dtype = BF16 if arr.dtype == np.uint16 else F32
@@ -175,7 +204,7 @@ def compress(arr: np.ndarray, p: Params, threads: int = 0):
     dims, n = _shape(arr.shape)
     nw = max_words(arr.shape, p)
     out = np.zeros(nw, dtype=np.uint64)
-    L = lib()
+    L = L or lib()
     if threads and threads > 1:
         bits = L.orc_compress_mt(arr.ctypes.data, dtype, dims, n, None, C.byref(p), _p(out, C.c_uint64), nw,
                                  threads)

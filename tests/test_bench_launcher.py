@@ -1,0 +1,41 @@
+"""bench.py's launcher and timing harness on the CPU (--stub: gloo, a trivial step instead of the encode).
+
+`python bench.py --gpus N` without a torchrun environment must start N ranks itself (one process per GPU, before
+the parent touches the GPU), each seeing RANK / LOCAL_RANK / WORLD_SIZE, and rank 0 must print one JSON line with
+n_gpus = N (--gpus was parsed and ignored)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*extra, env=None):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--stub", "--steps", "3", "--warmup", "1",
+           "--values", "4096", *extra]
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_self_launches_n_ranks(n):
+    d = _run("--gpus", str(n))
+    assert d["n_gpus"] == n
+    assert sorted(tuple(r[:3]) for r in d["ranks"]) == [(i, i, n) for i in range(n)]
+    assert all(r[3] == "self" for r in d["ranks"])
+    assert d["steps"] == 3 and d["warmup"] == 1 and d["ms_per_step"] > 0
+
+
+def test_bench_single_rank():
+    d = _run("--gpus", "1")
+    assert d["n_gpus"] == 1 and d["ranks"] == [[0, 0, 1, "torchrun"]]

@@ -1,16 +1,21 @@
-"""The N>1 exchange protocol (gcow_amd/dist.py) on world_size 2 / 3 gloo process groups on the CPU.
+"""The N>1 exchange code on world_size 2 / 3 (and 8 for empty shards) gloo process groups on the CPU.
 
-Each rank encodes its block-aligned shard with the oracle (CPU stand-in for the device encoder), then runs the same
-all-gather / stitch protocol the GPU path runs over RCCL; the rebuilt stream must equal the single-stream encode
-of the whole bucket, byte for byte (fixed and variable rate, ragged shards)."""
+The product functions run exactly as written -- gcow_amd.dist.encode_allgather / allgather_variable and both
+gcow_amd.ddp hooks -- with only their codec calls injected: tests/oracle_codec.OracleCodec does the encoding,
+stitching and decoding with the oracle on CPU tensors. The rebuilt stream must equal the oracle's single-stream
+encode of the whole bucket, byte for byte (fixed and variable rate, fp32 and bf16, ragged and empty shards); the
+hooks' gradients must equal the mean over ranks of the oracle's decode(encode(local gradient)), bit for bit."""
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -21,72 +26,136 @@ def _free_port():
     return p
 
 
-def np_stitch(dst, off, src, bits):
-    """CPU model of k_stitch: OR `bits` bits of src into dst at bit offset off."""
-    d = dst.numpy().view(np.uint64)
-    s = src.numpy().view(np.uint64)
-    nsw = (bits + 63) // 64
-    w0, w1 = off // 64, (off + bits + 63) // 64
-    for w in range(w0, w1):
-        sbit = 64 * w - off
-        if sbit < 0:
-            v = int(s[0]) << (-sbit)
-        else:
-            i, sh = sbit // 64, sbit % 64
-            v = int(s[i]) >> sh
-            if sh and i + 1 < nsw:
-                v |= int(s[i + 1]) << (64 - sh)
-        lo = 64 * w
-        if off + bits < lo + 64:
-            v &= (1 << (off + bits - lo)) - 1
-        d[w] = np.uint64(int(d[w]) | (v & (2 ** 64 - 1)))
+def _init(rank, world, port):
+    for p in (ROOT, os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
 
 
-def _worker(rank, world, port, mode, nvals, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _run(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    bad = [r for r in res if r[1] is not True]
+    assert not bad, bad
+    return res
+
+
+def _params(mode):
+    from gcow_amd import codec
+    return {"rate16": codec.rate(16, 1), "rate8": codec.rate(8, 1), "rate2.5": codec.rate(2.5, 1),
+            "acc1e-6": codec.accuracy(1e-6), "acc1e-3": codec.accuracy(1e-3), "prec20": codec.precision(20)}[mode]
+
+
+def _allgather_worker(rank, world, port, q, mode, nvals, bf16):
+    _init(rank, world, port)
     try:
-        import sys
-        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from gcow_amd import dist as gdist
         from oracle import oracle as O
+        from oracle_codec import OracleCodec
         a = O.gen_normal(nvals, 1e-3, 77, True)
-        p = O.rate(16, 1) if mode == "fixed" else O.accuracy(1e-6)
-        lo, hi = gdist.shard_bounds(nvals, world, rank)
-        w, bits = O.compress(a[lo:hi], p)
-        words = torch.from_numpy(np.concatenate([w, np.zeros(2, np.uint64)]).view(np.int64))
-        if mode == "fixed":
-            out = gdist.allgather_fixed(words, (hi - lo) // 4, p.maxbits)
-            total = out.numel() * 64
+        if bf16:
+            a = (a.view(np.uint32) >> 16).astype(np.uint16)
+            bucket = torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16)
         else:
-            out, total = gdist.allgather_variable(words, bits, stitch=np_stitch)
-        ref, ref_bits = O.compress(a, p)
-        ok = out.numpy().view(np.uint64)[: len(ref)].tobytes() == ref.tobytes()
-        ok = ok and (total == ref_bits if mode != "fixed" else total >= ref_bits)
-        q.put((rank, ok))
+            bucket = torch.from_numpy(a.copy())
+        p = _params(mode)
+        cdc = OracleCodec()
+        out, total = gdist.encode_allgather(bucket, p, codec=cdc)
+        ref, ref_bits = O.compress(a, O.expert(*p.tuple()))
+        got = out.numpy().view(np.uint64)
+        ok = total == ref_bits and got.size == ref.size and got.tobytes() == ref.tobytes()
+        lo, hi = gdist.shard_bounds(nvals, world, rank)
+        encoded = [r for r in cdc.records if r[0] == "encode"]
+        ok = ok and (len(encoded) == (1 if hi > lo else 0))  # an empty shard joins the exchange without encoding
+        q.put((rank, True if ok else ("mismatch", total, ref_bits, got.size, ref.size)))
+    except Exception as ex:  # pragma: no cover - reported through the queue
+        q.put((rank, repr(ex)))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode,nvals", [(2, "fixed", 4 * 4096), (2, "variable", 4 * 5003 + 2),
-                                               (3, "variable", 4 * 3001), (2, "variable", 6)])
-def test_allgather_protocol_gloo(world, mode, nvals):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, nvals, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=120) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-    assert all(ok for _, ok in res), res
+@pytest.mark.parametrize("world,mode,nvals,bf16", [
+    (2, "rate16", 4 * 4096, False),       # equal aligned shards: one all-gather is the stream
+    (3, "rate16", 4 * 3001 + 2, False),   # ragged shards: stitched at nb * maxbits offsets
+    (2, "rate2.5", 4 * 999, False),       # maxbits 10: shard ends inside a word
+    (2, "acc1e-6", 4 * 5003 + 2, False),
+    (3, "acc1e-6", 4 * 3001, False),
+    (3, "acc1e-3", 4 * 2000 + 1, True),   # bf16 variable rate (C5 shape, small)
+    (2, "prec20", 6, False),              # one rank holds the whole tiny bucket
+    (8, "acc1e-6", 400, False),           # world > nblocks / 16: ranks 7.. have empty shards (no hang)
+    (8, "rate16", 400, False),
+])
+def test_encode_allgather_gloo(world, mode, nvals, bf16):
+    _run(_allgather_worker, world, mode, nvals, bf16)
+
+
+def _hook_worker(rank, world, port, q, hook_name, mode):
+    _init(rank, world, port)
+    try:
+        import torch.nn as nn
+        from gcow_amd import ddp
+        from oracle import oracle as O
+        from oracle_codec import OracleCodec
+        torch.manual_seed(0)
+        model = nn.Linear(53, 37, bias=False)  # one parameter: the bucket is its flattened gradient (1961 values)
+        ref = nn.Linear(53, 37, bias=False)
+        ref.load_state_dict(model.state_dict())
+        dm = nn.parallel.DistributedDataParallel(model)
+        p = _params(mode)
+        dm.register_comm_hook(ddp.GcowHookState(params=p, codec=OracleCodec()), getattr(ddp, hook_name))
+        torch.manual_seed(100 + rank)  # a different batch per rank
+        x = torch.randn(16, 53)
+        dm(x).square().mean().backward()
+        ref(x).square().mean().backward()
+        local = ref.weight.grad.reshape(-1).contiguous()
+        allg = [torch.empty_like(local) for _ in range(world)]
+        dist.all_gather(allg, local)
+        op = O.expert(*p.tuple())
+        if hook_name == "compressed_allgather_hook":
+            acc = np.zeros(local.numel(), np.float32)
+            for g in allg:
+                w, _ = O.compress(g.numpy(), op)
+                acc = acc + O.decompress(w, (local.numel(),), op)
+            want = acc / np.float32(world)
+        else:  # the reference's order: mean all-reduce (x / world summed), then encode -> decode
+            mean = allg[0] / world
+            for g in allg[1:]:
+                mean = mean + g / world  # world 2: exact in any order (halving is exact)
+            w, _ = O.compress(mean.numpy(), op)
+            want = O.decompress(w, (local.numel(),), op)
+        got = dm.module.weight.grad.reshape(-1).numpy()
+        ok = np.array_equal(got.view(np.uint32), want.view(np.uint32))
+        q.put((rank, True if ok else "gradient != mean of oracle decode(encode(local grads))"))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("mode", ["rate16", "acc1e-6", "rate2.5"])
+def test_compressed_allgather_hook_gloo(world, mode):
+    """The hook body end to end over gloo: encode, length exchange, padded stream + index all-gather, one
+    decode-mean; bit-exact against the oracle's mean of decode(encode(each rank's gradient))."""
+    _run(_hook_worker, world, "compressed_allgather_hook", mode)
+
+
+@pytest.mark.parametrize("mode", ["rate16", "acc1e-6"])
+def test_roundtrip_hook_gloo(mode):
+    _run(_hook_worker, 2, "roundtrip_hook", mode)
 
 
 def test_shard_bounds_cover_and_align():
     from gcow_amd.dist import shard_bounds
-    for nvals in (1, 4, 7, 4096, 268435456, 10 ** 6 + 3):
+    for nvals in (1, 4, 7, 400, 4096, 268435456, 10 ** 6 + 3):
         for world in (1, 2, 3, 4, 8):
             b = [shard_bounds(nvals, world, r) for r in range(world)]
             assert b[0][0] == 0 and b[-1][1] == nvals
@@ -96,13 +165,31 @@ def test_shard_bounds_cover_and_align():
                 assert (hi - lo) % 64 == 0 or hi == nvals  # 16 blocks: 64-bit aligned at rate >= 1/4
 
 
+def test_oracle_codec_stitch_model():
+    """The CPU stand-in's stitch equals the oracle's single stream (sanity of the test double itself)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import oracle as O
+    from oracle_codec import OracleCodec
+    a = O.gen_normal(4 * 777 + 1, 1e-3, 5, True)
+    op = O.accuracy(1e-5)
+    cuts = [0, 4 * 100, 4 * 100, 4 * 500, a.size]
+    shards = [O.compress(a[x:y], op) for x, y in zip(cuts, cuts[1:])]
+    maxw = max(len(w) for w, _ in shards) + 1
+    src = np.zeros(maxw * len(shards), np.uint64)
+    for r, (w, _) in enumerate(shards):
+        src[r * maxw:r * maxw + len(w)] = w
+    lens = torch.tensor([b for _, b in shards], dtype=torch.int64)
+    total = int(lens.sum())
+    dst = torch.full(((total + 63) // 64,), -1, dtype=torch.int64)
+    OracleCodec().stitch_shards(dst, torch.from_numpy(src.view(np.int64)), maxw, lens, len(shards))
+    ref, bits = O.compress(a, op)
+    assert bits == total and dst.numpy().view(np.uint64).tobytes() == ref.tobytes()
+
 
 def _ddp_register(rank, world, port, q):
-    import sys
-    import torch.nn as nn
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    _init(rank, world, port)
     try:
+        import torch.nn as nn
         from gcow_amd import ddp
         for h in (ddp.roundtrip_hook, ddp.compressed_allgather_hook):
             m = nn.parallel.DistributedDataParallel(nn.Linear(4, 4))
@@ -115,14 +202,5 @@ def _ddp_register(rank, world, port, q):
 
 
 def test_ddp_hooks_register():
-    """gcow_amd.ddp hooks pass DDP's comm-hook signature check (compute runs in the -m gpu DDP tests)."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_ddp_register, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=120) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-    assert all(ok is True for _, ok in res), res
+    """gcow_amd.ddp hooks pass DDP's comm-hook signature check."""
+    _run(_ddp_register, 2)

@@ -1,0 +1,259 @@
+"""GPU parity of the multi-GPU exchange path against the oracle, bit-exact.
+
+* gcow_stitch_shards_device (one launch for every shard) vs the oracle's single-stream encode of the whole bucket;
+* gcow_decode_mean_device (one launch decodes every rank's stream and averages) vs the oracle's decodes summed in
+  rank order;
+* the product exchange code (gcow_amd.dist.encode_allgather, gcow_amd.ddp.compressed_allgather_hook) in 2 and 3
+  processes sharing the one GPU: the collectives run over gloo on host copies, every codec call runs the gfx950
+  kernels (a host-staging wrapper around gcow_amd.dist.DeviceCodec);
+* both DDP hooks at world 1 over RCCL, each gradient compared bit-exactly with the oracle.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def gc():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a device")
+    from gcow_amd import codec
+    return codec
+
+
+def _P(gc, op):
+    return gc.expert(*op.tuple())
+
+
+def _bucket(orc, n, seed, bf16=False):
+    a = orc.gen_normal(n, 1e-3, seed, True)
+    if bf16:
+        a = (a.view(np.uint32) >> 16).astype(np.uint16)
+    return a
+
+
+def _dev(a):
+    x = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return x.view(torch.bfloat16) if a.dtype == np.uint16 else x
+
+
+# ---------------------------------------------------------------------------------------------- stitch_shards
+@pytest.mark.parametrize("mode", ["acc1e-6", "acc1e-3_bf16", "rate2.5", "prec20"])
+@pytest.mark.parametrize("k", [2, 3, 8])
+def test_stitch_shards_equals_single_stream(gc, orc, mode, k):
+    """Shards cut at 16-block multiples (and one empty shard) encoded on the device separately, laid out shard_words
+    apart as after a padded all-gather, stitched in one launch == the oracle's stream of the whole bucket."""
+    bf16 = mode.endswith("bf16")
+    a = _bucket(orc, 4 * 10001 + 3, 11 + k, bf16)
+    op = {"acc1e-6": orc.accuracy(1e-6), "acc1e-3_bf16": orc.accuracy(1e-3), "rate2.5": orc.rate(2.5, 1),
+          "prec20": orc.precision(20)}[mode]
+    nb = (a.size + 3) // 4
+    per = (nb // k + 15) // 16 * 16
+    cuts = [min(4 * per * r, a.size) for r in range(k)] + [a.size]
+    if k >= 3:
+        cuts[1] = cuts[0]  # an empty shard
+    x = _dev(a)
+    enc = [gc.encode(x[lo:hi], _P(gc, op)) if hi > lo else None for lo, hi in zip(cuts, cuts[1:])]
+    lens = [e.bits if e is not None else 0 for e in enc]
+    maxw = max(1, max((b + 63) // 64 for b in lens))
+    src = torch.zeros(k * maxw, dtype=torch.int64, device="cuda")
+    for r, e in enumerate(enc):
+        if e is not None and lens[r]:
+            src[r * maxw:r * maxw + e.nwords] = e.stream()
+    total = sum(lens)
+    dst = torch.full(((total + 63) // 64,), -1, dtype=torch.int64, device="cuda")  # written whole, no zeroing
+    gc.stitch_shards(dst, src, maxw, torch.tensor(lens, dtype=torch.int64, device="cuda"))
+    ref, bits = orc.compress(a, op)
+    torch.cuda.synchronize()
+    assert total == bits
+    assert dst.cpu().numpy().view(np.uint64).tobytes() == ref.tobytes()
+
+
+# ---------------------------------------------------------------------------------------------- decode_mean
+def _oracle_mean(orc, streams, op, n):
+    acc = np.zeros(n, np.float32)
+    for w in streams:
+        acc = acc + orc.decompress(w, (n,), op)
+    return acc / np.float32(len(streams))
+
+
+@pytest.mark.parametrize("mode", ["rate16", "rate8", "rate2.5", "expert_generic", "acc1e-6", "acc1e-3", "bf16_acc1e-6"])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_decode_mean_vs_oracle(gc, orc, mode, world):
+    n = 4 * 20001 + 2  # a partial last block; > 128 index chunks
+    op = {"rate16": orc.rate(16, 1), "rate8": orc.rate(8, 1), "rate2.5": orc.rate(2.5, 1),
+          "expert_generic": orc.expert(64, 64, 20, -1074), "acc1e-6": orc.accuracy(1e-6),
+          "acc1e-3": orc.accuracy(1e-3), "bf16_acc1e-6": orc.accuracy(1e-6)}[mode]
+    fixed = op.minbits == op.maxbits
+    buckets = [_bucket(orc, n, 900 + r, mode.startswith("bf16")) for r in range(world)]
+    encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else 16) for b in buckets]
+    lens = [e.bits for e in encs]
+    sw = max((b + 63) // 64 for b in lens) + (0 if fixed else 1)
+    streams = torch.zeros(world * sw + 2, dtype=torch.int64, device="cuda")
+    for r, e in enumerate(encs):
+        streams[r * sw:r * sw + e.nwords] = e.stream()
+    idx, ni = None, 0
+    if not fixed:
+        ni = encs[0].index.numel()
+        idx = torch.cat([e.index[:ni] for e in encs])
+    got = gc.decode_mean(streams, sw, world, n, _P(gc, op), idx, ni, 0 if fixed else 16)
+    want = _oracle_mean(orc, [orc.compress(b, op)[0] for b in buckets], op, n)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+# ---------------------------------------------------------------------------------------------- multi-process
+class HostStagedDeviceCodec:
+    """gcow_amd.dist.DeviceCodec behind host copies: the exchange code moves CPU tensors over gloo (two processes
+    cannot share one GPU over RCCL), every codec call runs the device kernels."""
+
+    def __init__(self):
+        from gcow_amd.dist import DeviceCodec
+        self.d = DeviceCodec()
+        self.calls = []
+
+    def encode(self, x, params, index_stride=0):
+        w, b, i = self.d.encode(x.cuda(), params, index_stride)
+        self.calls.append("encode")
+        return w.cpu(), b.cpu(), (i.cpu() if i is not None else None)
+
+    def stitch_shards(self, dst, src, shard_words, lens, nshards):
+        dd = dst.cuda()
+        self.d.stitch_shards(dd, src.cuda(), shard_words, lens.cuda(), nshards)
+        dst.copy_(dd.cpu())
+        self.calls.append("stitch")
+        return dst
+
+    def decode(self, words, n, params, index=None, index_stride=0, out=None):
+        o = self.d.decode(words.cuda(), n, params, index.cuda() if index is not None else None, index_stride).cpu()
+        return out.copy_(o) if out is not None else o
+
+    def decode_mean(self, streams, stream_words, nstreams, n, params, index=None, index_words=0, index_stride=0,
+                    out=None):
+        o = self.d.decode_mean(streams.cuda(), stream_words, nstreams, n, params,
+                               index.cuda() if index is not None else None, index_words, index_stride).cpu()
+        self.calls.append("decode_mean")
+        return out.copy_(o) if out is not None else o
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _mp_worker(rank, world, port, q, what, mode):
+    import torch.distributed as dist
+    for p in (ROOT, os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    try:
+        from gcow_amd import codec, ddp
+        from gcow_amd import dist as gdist
+        from oracle import oracle as O
+        p = {"rate16": codec.rate(16, 1), "acc1e-6": codec.accuracy(1e-6), "bf16_acc1e-3": codec.accuracy(1e-3)}[mode]
+        op = O.expert(*p.tuple())
+        cdc = HostStagedDeviceCodec()
+        if what == "encode_allgather":
+            a = O.gen_normal(4 * 30011 + 1, 1e-3, 5, True)
+            if mode.startswith("bf16"):
+                a = (a.view(np.uint32) >> 16).astype(np.uint16)
+                bucket = torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16)
+            else:
+                bucket = torch.from_numpy(a.copy())
+            out, total = gdist.encode_allgather(bucket, p, codec=cdc)
+            ref, bits = O.compress(a, op)
+            ok = total == bits and out.numpy().view(np.uint64).tobytes() == ref.tobytes()
+        else:
+            import torch.nn as nn
+            torch.manual_seed(0)
+            model = nn.Linear(67, 61, bias=False)
+            refm = nn.Linear(67, 61, bias=False)
+            refm.load_state_dict(model.state_dict())
+            dm = nn.parallel.DistributedDataParallel(model)
+            dm.register_comm_hook(ddp.GcowHookState(params=p, codec=cdc), ddp.compressed_allgather_hook)
+            torch.manual_seed(10 + rank)
+            x = torch.randn(8, 67)
+            dm(x).square().mean().backward()
+            refm(x).square().mean().backward()
+            g = refm.weight.grad.reshape(-1).contiguous()
+            allg = [torch.empty_like(g) for _ in range(world)]
+            dist.all_gather(allg, g)
+            acc = np.zeros(g.numel(), np.float32)
+            for t in allg:
+                acc = acc + O.decompress(O.compress(t.numpy(), op)[0], (g.numel(),), op)
+            want = acc / np.float32(world)
+            got = dm.module.weight.grad.reshape(-1).numpy()
+            ok = np.array_equal(got.view(np.uint32), want.view(np.uint32)) and "decode_mean" in cdc.calls
+        q.put((rank, True if ok else "mismatch"))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("what,mode", [("encode_allgather", "rate16"), ("encode_allgather", "acc1e-6"),
+                                       ("encode_allgather", "bf16_acc1e-3"), ("hook", "rate16"), ("hook", "acc1e-6")])
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_multiprocess_device_codec(gc, what, mode, world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mp_worker, args=(r, world, port, q, what, mode)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=60)
+    assert all(ok is True for _, ok in res), res
+
+
+# ---------------------------------------------------------------------------------------------- DDP hooks, RCCL
+@pytest.fixture
+def nccl_world1():
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("hook", ["roundtrip_hook", "compressed_allgather_hook"])
+@pytest.mark.parametrize("mode", ["rate16", "acc1e-6", "rate8"])
+def test_ddp_hooks_world1_bit_exact(gc, orc, nccl_world1, hook, mode):
+    """One rank over RCCL: the weight gradient (the whole bucket) equals the oracle's decode(encode(local grad)) --
+    (0 + x) / 1 for the all-gather hook -- bit for bit."""
+    from gcow_amd import ddp
+    params = {"rate16": gc.rate(16, 1), "acc1e-6": gc.accuracy(1e-6), "rate8": gc.rate(8, 1)}[mode]
+    torch.manual_seed(0)
+    model = torch.nn.Linear(64, 97, bias=False).cuda()
+    ref = torch.nn.Linear(64, 97, bias=False).cuda()
+    ref.load_state_dict(model.state_dict())
+    dm = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0])
+    dm.register_comm_hook(ddp.GcowHookState(params=params), getattr(ddp, hook))
+    x = torch.randn(32, 64, device="cuda")
+    dm(x).square().mean().backward()
+    ref(x).square().mean().backward()
+    g = ref.weight.grad.reshape(-1).cpu().numpy()
+    op = orc.expert(*params.tuple())
+    dec = orc.decompress(orc.compress(g, op)[0], g.shape, op)
+    want = (np.zeros_like(dec) + dec) / np.float32(1) if hook == "compressed_allgather_hook" else dec
+    got = model.weight.grad.reshape(-1).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

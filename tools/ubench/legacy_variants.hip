@@ -1,7 +1,58 @@
 // Historical 1-D fixed-rate encoder variants (lean / lean-2 / lean-3 coders, per-lane, lockstep, persistent and
-// non-persistent kernels) kept for the ablation microbenchmark only; the product uses k_encode_fixed1d_pipe with the
-// lean-4 coder (gcow_amd/csrc/gcow_kernels.hip). Included by ablate.hip after gcow_kernels.hip.
+// non-persistent kernels) kept for the ablation microbenchmark only; the product uses the one-shot
+// k_encode_fixed1d_np with the lean-5 coder (gcow_amd/csrc/gcow_kernels.hip). Included by ablate.hip after
+// gcow_kernels.hip.
 namespace gcow {
+
+// ---- the persistent grid-stride lean-5 encoder (the product kernel before the one-shot grid)
+// Persistent grid-stride encoder with NB rotating register buffers (prefetch depth NB): each step codes buffer k,
+// stores the block, then refills buffer k with the block NB strides ahead. In steady state the block coded next was
+// loaded NB steps ago and 2 (NB - 1) memory ops were issued after it, hence vmcnt(2 (NB - 1)). The caller keeps
+// (nfull + NB * stride) * bytes-per-block below 2^32 (chunked launches).
+template <int DT, uint32_t WB, int NB>
+__global__ __launch_bounds__(256) void k_encode_fixed1d_pipe(const void* __restrict__ in, uint32_t nfull, Params p,
+                                                             void* __restrict__ out)
+{
+  __shared__ uint32_t tab2[1280];
+#pragma unroll
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab2[t] = g_plane_tab5.v[t];
+  __syncthreads();
+  constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;  // input bytes per block
+  const pipe_v4i rin = buf_rsrc(in, nfull * IB), rout = buf_rsrc(out, nfull * (WB / 8));
+  const uint32_t stride = gridDim.x * 256u;
+  uint32_t b = blockIdx.x * 256u + threadIdx.x;
+  uint32_t bw = __builtin_amdgcn_readfirstlane(blockIdx.x * 256u + (threadIdx.x & ~63u));  // wave's first block
+  if (bw >= nfull) return;
+  typename PipeRow<DT>::T r[NB];
+#pragma unroll
+  for (int d = 0; d < NB; d++) r[d] = PipeRow<DT>::load((b + d * stride) * IB, rin);
+#pragma unroll
+  for (int d = 0; d < NB; d++) pipe_wait<0>(r[d]);
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      pipe_wait<2 * (NB - 1)>(r[k]);
+      float f[4];
+      PipeRow<DT>::unpack(r[k], f);
+      bool special;
+      uint64_t w = encode_block1d_lean5<WB>(f, tab2, special);
+      if (special) {
+        RegWriter64 rw{0ull, 0u};
+        encode_block<1>(rw, f, p);
+        w = WB == 64 ? rw.acc : (rw.acc & ((1ull << WB) - 1ull));
+      }
+      pipe_store<WB>(b * (WB / 8), rout, w);
+      r[k] = PipeRow<DT>::load((b + NB * stride) * IB, rin);
+      b += stride;
+      bw += stride;
+      if (bw >= nfull) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+      }
+    }
+  }
+}
+
 
 // ---- lean-4 coder and its pair table (the product default before the lean-5 coder)
 __host__ __device__ constexpr PlaneTab2 make_plane_tab2()
