@@ -404,6 +404,14 @@ __device__ __forceinline__ int32_t cvt_i32_hw(float x)
   return r;
 }
 
+// v_ffbh_u32 as an opaque instruction: count of leading zeros, all ones (not UB) for 0
+__device__ __forceinline__ uint32_t ffbh_hw(uint32_t x)
+{
+  uint32_t r;
+  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 // Pair-table lookup chained on the previous entry's row (n' << 10 is already a byte offset).
 __device__ __forceinline__ uint32_t tab5_next(const uint32_t* tab, uint32_t e, uint32_t byte)
 {
@@ -467,6 +475,119 @@ __device__ __forceinline__ uint64_t encode_block1d_lean5(const float* f, const u
   constexpr uint64_t TINY = tiny_payload_cx((int)WB - 9) << 9;
   const uint64_t tv = m ? (TINY | (2ull * E + 3ull)) : 0ull;
   acc = E < 29u ? tv : acc;  // zero, subnormal and tiny-normal maxima: every value casts to INT_MIN (or is 0)
+  return WB == 64 ? acc : (acc & ((1ull << WB) - 1ull));
+}
+
+// ---- lean-6: the 16-plane window from byte-indexed LDS tables instead of a shift/mask transpose.
+// With w_i = u_i << (31 - M0) (plane M0 at bit 31, planes below bit 0 shifted in as zeros), window nibble j holds bit
+// 31 - j of w_0..w_3: nibbles 0..7 come from the top bytes, 8..15 from the next bytes. Table i spreads byte b reversed
+// onto nibble bit i (bit k of b -> bit 4 (7 - k) + i), so each half-window is four lookups OR-ed together: 8 LDS reads
+// and 14 VALU per block where plane_window's bit reversals and four 64-bit delta swaps took ~45.
+struct SpreadTab {
+  uint32_t v[4 * 256];
+};
+
+__host__ __device__ constexpr SpreadTab make_rspread()
+{
+  SpreadTab T{};
+  for (uint32_t i = 0; i < 4; i++)
+    for (uint32_t b = 0; b < 256; b++) {
+      uint32_t r = 0;
+      for (uint32_t k = 0; k < 8; k++)
+        if ((b >> k) & 1u) r |= 1u << (4 * (7 - k) + i);
+      T.v[256 * i + b] = r;
+    }
+  return T;
+}
+
+__device__ const SpreadTab g_rspread = make_rspread();
+
+// entry t of the spread tables computed in a kernel prologue (no table load): byte t & 255 onto nibble bit t >> 8
+__device__ __forceinline__ uint32_t rspread_entry(uint32_t t)
+{
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; k++) v |= ((t >> k) & 1u) << (4 * (7 - k));
+  return v << (t >> 8);
+}
+
+// 16 planes from plane 31 of w (already shifted so the window's top plane is bit 31) down, as nibbles
+__device__ __forceinline__ uint64_t window_lds(const uint32_t* rs, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3)
+{
+  const uint32_t lo = rs[w0 >> 24] | rs[256 + (w1 >> 24)] | rs[512 + (w2 >> 24)] | rs[768 + (w3 >> 24)];
+  const uint32_t hi = rs[(w0 >> 16) & 255u] | rs[256 + ((w1 >> 16) & 255u)] | rs[512 + ((w2 >> 16) & 255u)] |
+                      rs[768 + ((w3 >> 16) & 255u)];
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// Lean-6 block: the lean-5 stream (encode.c:457-495 for d = 1, fixed rate, kmin = 0) with
+//  * the block maximum as a float max3 of |f| (NaN caught by two unordered compares: it never wins the maximum,
+//    encode.c:146-150, but it casts to INT_MIN, so such blocks take the generic coder);
+//  * the lift and the negabinary map fused, the map's add folded into the last lifting add where there is one;
+//  * the window from window_lds;
+//  * the group-phase end jg = clz(u2 | u3) - sh, with 31 for o23 = 0 (jg = M0);
+//  * zero blocks coded by the main path (u = 0 codes to all-zero bits after a zero header), so only tiny-normal and
+//    subnormal maxima (0 < E < 29) take the constant payload.
+template <uint32_t WB>
+__device__ __forceinline__ uint64_t encode_block1d_lean6(const float* f, const uint32_t* tab, const uint32_t* rs,
+                                                         bool& special)
+{
+  uint32_t m;  // max |f| as bits: v_max3_f32 / v_max_f32 with |.| modifiers (no canonicalising fmaxf)
+  asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(m) : "v"(f[0]), "v"(f[1]), "v"(f[2]));
+  asm("v_max_f32_e64 %0, %0, |%1|" : "+v"(m) : "v"(f[3]));
+  special = m >= 0x7f800000u || __builtin_isunordered(f[0], f[1]) || __builtin_isunordered(f[2], f[3]);
+  const uint32_t E = m >> 23;
+  const float s = __uint_as_float((283u - E) << 23);  // 2^(30 - e); meaningless for tiny / special lanes
+  uint32_t x = (uint32_t)cvt_i32_hw(f[0] * s), y = (uint32_t)cvt_i32_hw(f[1] * s);
+  uint32_t z = (uint32_t)cvt_i32_hw(f[2] * s), w = (uint32_t)cvt_i32_hw(f[3] * s);
+  // fwd_lift (encode.c:212-225), int32 wraparound; arithmetic shifts on the signed view
+  auto asr = [](uint32_t v) { return (uint32_t)((int32_t)v >> 1); };
+  constexpr uint32_t NB = 0xaaaaaaaau;
+  x = asr(x + w); w -= x;
+  z = asr(z + y); y -= z;
+  x = asr(x + z); z -= x;
+  w = asr(w + y); y -= w;
+  const uint32_t u3 = (w + asr(y) + NB) ^ NB;  // w += y >> 1, then the negabinary map
+  const uint32_t u1 = (y - asr(w + asr(y)) + NB) ^ NB;
+  const uint32_t u0 = (x + NB) ^ NB, u2 = (z + NB) ^ NB;
+  const uint32_t o23 = u2 | u3;
+  const uint32_t sh = __builtin_clz(u0 | u1 | o23 | 1u);  // 31 - M0
+  const int M0 = 31 - (int)sh;
+  const int jg = (int)min(ffbh_hw(o23), 31u) - (int)sh;  // group phase: window nibbles 0 .. jg (o23 = 0: M0)
+  const uint64_t Y = window_lds(rs, u0 << sh, u1 << sh, u2 << sh, u3 << sh);
+  uint32_t pos = 9 + sh;
+  uint32_t e = tab[(uint32_t)Y & 255u];
+  uint32_t G = e >> 17, gl = (e >> 13) & 15u;
+  int j = 2;
+  if (__any(jg >= 2)) {
+    e = tab5_next(tab, e, ((uint32_t)Y >> 8) & 255u);
+    G |= (e >> 17) << gl;
+    gl += (e >> 13) & 15u;
+    j = 4;
+  }
+  const uint32_t hdr = m ? 2u * E + 3u : 0u;  // zero block: a single 0 bit, every later bit 0 as well
+  uint64_t acc = (uint64_t)hdr | ((uint64_t)G << pos);
+  pos += gl;
+#pragma unroll
+  for (int jj = 4; jj < 16; jj += 2) {
+    if (j < jj || !__any(jj <= jg)) break;
+    e = tab5_next(tab, e, (uint32_t)(Y >> (4 * jj)) & 255u);
+    const uint32_t code = pos < WB ? (e >> 17) : 0u;  // 64-bit shifts wrap: nothing past the budget
+    acc |= (uint64_t)code << pos;
+    pos += (e >> 13) & 15u;
+    j = jj + 2;
+  }
+  const bool tiny = m - 1u < (29u << 23) - 1u;  // 0 < E < 29: tiny-normal and subnormal maxima (coded below)
+  special = special || (!tiny && jg >= 16 && pos < WB);  // group phase runs past the 16-plane window
+  if (j < 16 && pos < WB) acc |= (Y >> (4 * j)) << pos;  // rest of the window, verbatim
+  const uint32_t p2 = pos + 4u * (uint32_t)(16 - j);      // where plane M0 - 16 lands
+  if (__any(p2 < WB && M0 >= 16)) {
+    const uint32_t s2 = sh + 16u;  // <= 31 where used (M0 >= 16)
+    const uint64_t Y2 = window_lds(rs, u0 << s2, u1 << s2, u2 << s2, u3 << s2);  // planes M0-16 .. M0-31
+    if (p2 < WB && M0 >= 16) acc |= Y2 << p2;
+  }
+  constexpr uint64_t TINY = tiny_payload_cx((int)WB - 9) << 9;
+  acc = tiny ? (TINY | hdr) : acc;  // every value casts to INT_MIN
   return WB == 64 ? acc : (acc & ((1ull << WB) - 1ull));
 }
 
@@ -541,19 +662,22 @@ __device__ __forceinline__ void pipe_store(uint32_t off, pipe_v4i rs, uint64_t w
 // (vmcnt counts loads and stores together, in issue order). Out-of-range lanes read zeros and their stores are
 // dropped by the buffer range check, so control flow stays wave-uniform. Measured against the persistent grid-stride
 // pipeline above, the one-shot shape streams HBM like a plain copy kernel.
-template <int DT, uint32_t WB, int U>
-__global__ __launch_bounds__(256) void k_encode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
-                                                           void* __restrict__ out)
+template <int DT, uint32_t WB, int U, uint32_t T = 256>
+__global__ __launch_bounds__(T) void k_encode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
+                                                         void* __restrict__ out)
 {
-  __shared__ uint32_t tab[1280];
+  __shared__ uint32_t tab[1280 + 1024];  // pair table, then the four window spread tables
   constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;  // input bytes per block
   const pipe_v4i rin = buf_rsrc(in, nfull * IB), rout = buf_rsrc(out, nfull * (WB / 8));
-  const uint32_t b0 = blockIdx.x * (256u * U) + threadIdx.x;
+  const uint32_t b0 = blockIdx.x * (T * U) + threadIdx.x;
   typename PipeRow<DT>::T r[U];
 #pragma unroll
-  for (int k = 0; k < U; k++) r[k] = PipeRow<DT>::load((b0 + 256u * k) * IB, rin);
+  for (int k = 0; k < U; k++) r[k] = PipeRow<DT>::load((b0 + T * k) * IB, rin);
 #pragma unroll
-  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab[t] = g_plane_tab5.v[t];
+  for (uint32_t t = threadIdx.x; t < 1280; t += T) tab[t] = g_plane_tab5.v[t];
+  // the spread tables are computed, not loaded: entry 256 i + b = byte b reversed onto nibble bit i
+#pragma unroll
+  for (uint32_t t = threadIdx.x; t < 1024; t += T) tab[1280 + t] = rspread_entry(t);
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < U; k++) {
@@ -561,13 +685,13 @@ __global__ __launch_bounds__(256) void k_encode_fixed1d_np(const void* __restric
     float f[4];
     PipeRow<DT>::unpack(r[k], f);
     bool special;
-    uint64_t w = encode_block1d_lean5<WB>(f, tab, special);
+    uint64_t w = encode_block1d_lean6<WB>(f, tab, tab + 1280, special);
     if (special) {
       RegWriter64 rw{0ull, 0u};
       encode_block<1>(rw, f, p);
       w = WB == 64 ? rw.acc : (rw.acc & ((1ull << WB) - 1ull));
     }
-    pipe_store<WB>((b0 + 256u * k) * (WB / 8), rout, w);
+    pipe_store<WB>((b0 + T * k) * (WB / 8), rout, w);
   }
 }
 
@@ -781,7 +905,8 @@ __global__ __launch_bounds__(T) void k_encode_tiles(FieldDesc F, Params p, uint3
 // group phase longer than 16 planes or 64 bits -> generic coder.
 template <bool CODE>
 __device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uint16_t* tab, const uint32_t* tab2,
-                                                      int minexp, uint32_t maxprec, uint64_t* c, bool& special)
+                                                      const uint32_t* rs, int minexp, uint32_t maxprec, uint64_t* c,
+                                                      bool& special)
 {
   const uint32_t a0 = __float_as_uint(f[0]) & 0x7fffffffu, a1 = __float_as_uint(f[1]) & 0x7fffffffu;
   const uint32_t a2 = __float_as_uint(f[2]) & 0x7fffffffu, a3 = __float_as_uint(f[3]) & 0x7fffffffu;
@@ -808,7 +933,8 @@ __device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uin
   const uint32_t pos0 = 9u + (uint32_t)(31 - max(M0, kmin - 1));  // header + empty planes
   const int nplanes = max(M0 - kmin + 1, 0);                        // planes M0 .. kmin
   const int jg = M0 - max(T2, kmin);                                 // last group-phase plane (window index)
-  const uint64_t Y = plane_window(u, (uint32_t)(31 - M0));
+  const uint32_t sh = (uint32_t)(31 - M0);  // M0 >= 0: the |1 in the clz
+  const uint64_t Y = window_lds(rs, u[0] << sh, u[1] << sh, u[2] << sh, u[3] << sh);
   uint64_t g = 0;  // group-phase bits, relative to pos0
   uint32_t glen = 0, n = 0;
   int j = 0;
@@ -842,7 +968,8 @@ __device__ __forceinline__ uint32_t encode_block1d_var(const float* f, const uin
     c[1] = pos0 ? g >> (64 - pos0) : 0ull;  // pos0 >= 9
     if (tplanes > 0) {
       // tail nibbles j .. nplanes-1 of the 32-plane window (Y, then planes M0-16 .. M0-31)
-      const uint64_t Y2 = nplanes > 16 ? plane_window(u, (uint32_t)min(47 - M0, 31)) : 0ull;
+      const uint32_t s2 = sh + 16u;  // <= 31 where used (nplanes > 16 needs M0 >= 16)
+      const uint64_t Y2 = nplanes > 16 ? window_lds(rs, u[0] << s2, u[1] << s2, u[2] << s2, u[3] << s2) : 0ull;
       // j is the wave-uniform group-loop count, 1..16 (16 when another lane's group phase filled the window)
       uint64_t t0 = j == 16 ? Y2 : (Y >> (4 * j)) | (Y2 << (64 - 4 * j));
       uint64_t t1 = j == 16 ? 0ull : Y2 >> (4 * j);
@@ -1014,10 +1141,12 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
   __shared__ uint32_t scan_sh[T / 64];
   __shared__ uint16_t tab[80];
   __shared__ uint32_t tab2[1280];
+  __shared__ uint32_t rs[1024];  // window spread tables (window_lds)
   uint32_t* lds = (uint32_t*)lds64;
   const uint32_t tid = threadIdx.x;
   if (tid < 80) tab[tid] = plane_entry4(tid);
   for (uint32_t t = tid; t < 1280; t += T) tab2[t] = g_plane_tab5.v[t];
+  for (uint32_t t = tid; t < 1024; t += T) rs[t] = rspread_entry(t);
   const uint64_t b0 = (uint64_t)blockIdx.x * range;
   const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
   const bool final_range = b1 == F.nblocks;
@@ -1076,7 +1205,7 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
 #pragma unroll
     for (int k = 0; k < U; k++) {
       const bool valid = t0 + (uint64_t)tid * U + k < b1;
-      len[k] = encode_block1d_var<true>(f[k], tab, tab2, p.minexp, p.maxprec, c[k], sp[k]);
+      len[k] = encode_block1d_var<true>(f[k], tab, tab2, rs, p.minexp, p.maxprec, c[k], sp[k]);
       sp[k] = sp[k] && valid;
       if (sp[k]) {
         len[k] = count_block<1>(f[k], p);
@@ -2284,7 +2413,7 @@ static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, vo
         const uint32_t nc = min(CH, nfull - c0);
         const void* ic = (const char*)in + (size_t)c0 * IB;
         void* oc = (char*)out + (size_t)c0 * (WB / 8);
-        k_encode_fixed1d_np<DT, WB, 8><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
+        k_encode_fixed1d_np<DT, WB, 8, 256><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
       }
     }
   }

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Short, fixed-count runs of the C3 / C5 encoders for rocprofv3 kernel traces and PMC passes (few dispatches, so
-a counter pass stays within seconds).  usage: prof_cases.py [c3] [c5] [--reps N]"""
+a counter pass stays within seconds).  usage: prof_cases.py [c2] [c3] [c5] [--reps N]"""
 import argparse
 import math
 import os
@@ -11,6 +11,16 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from gcow_amd import codec  # noqa: E402
+
+
+def c2(reps):
+    n = 256 << 20
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    codec.fill_normal(x)
+    enc = codec.Encoder((n,), torch.float32, codec.rate(16, 1))
+    for _ in range(reps):
+        enc(x)
+    torch.cuda.synchronize()
 
 
 def c3(reps):

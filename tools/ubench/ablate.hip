@@ -739,6 +739,48 @@ __global__ __launch_bounds__(256) void k_c3_split(FieldDesc F, Params p, uint32_
   uint32_t* dst = out32 + (uint64_t)b0 * WPB;
   for (uint32_t j = tid; j < nvalid * WPB; j += 256) dst[j] = lds_w[(j / WPB) * (WPB + 1) + (j % WPB)];
 }
+
+// Diagnostic build of k_encode_fixed1d_np<F32, 64, 8> (same body) with per-workgroup clock stamps: s_memtime /
+// s_memrealtime at entry and after the last store, written by thread 0 with a vector store into a stamp buffer that
+// no other code reads. In-kernel clock = d(memtime) / d(memrealtime) x 100 MHz (MI355X_MICROARCH.md DVFS item 6).
+__global__ __launch_bounds__(256) void k_np6_stamp(const void* __restrict__ in, uint32_t nfull, Params p,
+                                                   void* __restrict__ out, uint64_t* __restrict__ stamps)
+{
+  constexpr int U = 8;
+  constexpr uint32_t WB = 64;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  __shared__ uint32_t tab[1280 + 256];
+  const pipe_v4i rin = buf_rsrc(in, nfull * 16u), rout = buf_rsrc(out, nfull * 8u);
+  const uint32_t b0 = blockIdx.x * (256u * U) + threadIdx.x;
+  typename PipeRow<DT_F32>::T r[U];
+#pragma unroll
+  for (int k = 0; k < U; k++) r[k] = PipeRow<DT_F32>::load((b0 + 256u * k) * 16u, rin);
+#pragma unroll
+  for (uint32_t t = threadIdx.x; t < 1280; t += 256) tab[t] = g_plane_tab5.v[t];
+  tab[1280 + threadIdx.x] = g_rspread.v[threadIdx.x];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    pipe_wait<U - 1>(r[k]);
+    float f[4];
+    PipeRow<DT_F32>::unpack(r[k], f);
+    bool special;
+    uint64_t w = encode_block1d_lean6<WB>(f, tab, tab + 1280, special);
+    if (special) {
+      RegWriter64 rw{0ull, 0u};
+      encode_block<1>(rw, f, p);
+      w = rw.acc;
+    }
+    pipe_store<WB>((b0 + 256u * k) * 8u, rout, w);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    uint64_t* s4 = stamps + 4ull * blockIdx.x;
+    s4[0] = t0; s4[1] = t1; s4[2] = r0; s4[3] = r1;
+  }
+}
 }  // namespace gcow
 
 static gcow::FieldDesc c3_field(const void* in)
@@ -753,11 +795,32 @@ static gcow::FieldDesc c3_field(const void* in)
   return F;
 }
 
+static uint64_t* g_stamps = nullptr;
+static const size_t kStampLaunches = 32, kStampWgs = 1u << 16;
+
+// stamps of launch i of mode 90 (k_np6_stamp): 4 uint64 per workgroup, kStampWgs workgroups per launch slot
+extern "C" int ablate_stamp_copy(void* host, int launch, size_t wgs)
+{
+  if (!g_stamps) return -1;
+  return (int)hipMemcpy(host, g_stamps + (size_t)launch * kStampWgs * 4, wgs * 32, hipMemcpyDeviceToHost);
+}
+
 extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, int wgs, void* stream)
 {
+  if (mode == 90) {  // wgs = launch slot
+    if (!g_stamps && hipMalloc((void**)&g_stamps, kStampLaunches * kStampWgs * 32) != hipSuccess) return -1;
+    const uint32_t g = (nfull + 2047) / 2048;
+    if (g > kStampWgs || wgs < 0 || (size_t)wgs >= kStampLaunches) return -2;
+    gcow::k_np6_stamp<<<g, 256, 0, (hipStream_t)stream>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out,
+                                                           g_stamps + (size_t)wgs * kStampWgs * 4);
+    return (int)hipGetLastError();
+  }
   const uint32_t grid = min((nfull + 255) / 256, (uint32_t)(256 * wgs));
   hipStream_t st = (hipStream_t)stream;
   switch (mode) {
+    case 91: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64, 8, 256><<<(nfull + 2047) / 2048, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 92: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64, 8, 512><<<(nfull + 4095) / 4096, 512, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 93: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64, 8, 1024><<<(nfull + 8191) / 8192, 1024, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 0: gcow::k_ablate<0><<<grid, 256, 0, st>>>((const float4*)in, nfull, (uint64_t*)out); break;
     case 1: gcow::k_ablate<1><<<grid, 256, 0, st>>>((const float4*)in, nfull, (uint64_t*)out); break;
     case 2: gcow::k_ablate<2><<<grid, 256, 0, st>>>((const float4*)in, nfull, (uint64_t*)out); break;
@@ -788,7 +851,7 @@ extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, i
     case 20: gcow::k_np1<2><<<(nfull + 511) / 512, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
     case 21: gcow::k_np1<4><<<(nfull + 1023) / 1024, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
     case 22: gcow::k_p1<<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
-    case 23: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64><<<(nfull + 255) / 256, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 23: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64, 1, 256><<<(nfull + 255) / 256, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 24: gcow::k_pd<2><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
     case 25: gcow::k_pd<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
     case 26: gcow::k_pd<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, (uint64_t*)out); break;
