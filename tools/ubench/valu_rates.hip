@@ -22,6 +22,7 @@ __global__ __launch_bounds__(256) void k_rate(uint32_t iters, uint64_t* out, uin
   uint32_t a0 = threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 * 11, a5 = a0 * 13, a6 = a0 * 17,
            a7 = a0 * 19;
   uint64_t q0 = a0, q1 = a1, q2 = a2, q3 = a3;
+  if constexpr (OP == 16) asm volatile("s_mov_b64 s[20:21], 0x5555" ::: "s20", "s21");
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   for (uint32_t i = 0; i < iters; i++) {
     if constexpr (OP == 0) { CH8(OP1("v_add_u32")) CH8(OP1("v_add_u32")) }
@@ -47,6 +48,21 @@ __global__ __launch_bounds__(256) void k_rate(uint32_t iters, uint64_t* out, uin
     if constexpr (OP == 13) { CH8(OP1("v_lshlrev_b32")) CH8(OP1("v_lshlrev_b32")) }
     if constexpr (OP == 14) { CH8(OP3("v_add3_u32", "%0")) CH8(OP3("v_add3_u32", "%0")) }
     if constexpr (OP == 15) { CH8(OP3("v_perm_b32", "%0")) CH8(OP3("v_perm_b32", "%0")) }
+    if constexpr (OP == 16) { CH8(OP3("v_cndmask_b32_e64", "s[20:21]")) CH8(OP3("v_cndmask_b32_e64", "s[20:21]")) }
+    if constexpr (OP == 17) { CH8(OP1("v_sub_u32")) CH8(OP1("v_sub_u32")) }
+    if constexpr (OP == 18) { CH8(OP1("v_ashrrev_i32")) CH8(OP1("v_ashrrev_i32")) }
+    if constexpr (OP == 19) { CH8(OP3("v_and_or_b32", "%0")) CH8(OP3("v_and_or_b32", "%0")) }
+    if constexpr (OP == 20) { CH8(OP3("v_or3_b32", "%0")) CH8(OP3("v_or3_b32", "%0")) }
+    if constexpr (OP == 21) { CH8(OP1("v_and_b32")) CH8(OP1("v_and_b32")) }
+    if constexpr (OP == 22) { CH8(OP1("v_or_b32")) CH8(OP1("v_or_b32")) }
+    if constexpr (OP == 23) { CH8(OP1("v_min_u32")) CH8(OP1("v_min_u32")) }
+    if constexpr (OP == 24) { CH8(OP1("v_lshrrev_b32")) CH8(OP1("v_lshrrev_b32")) }
+    if constexpr (OP == 25) { CH8(OP3("v_max3_f32", "%0")) CH8(OP3("v_max3_f32", "%0")) }
+    if constexpr (OP == 26) {
+#define SDW(a, b) "v_lshlrev_b32_sdwa " a ", " b ", " a " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n"
+      CH8(SDW("%0", "%1") SDW("%1", "%2") SDW("%2", "%3") SDW("%3", "%4") SDW("%4", "%5") SDW("%5", "%6") SDW("%6", "%7") SDW("%7", "%0"))
+      CH8(SDW("%0", "%1") SDW("%1", "%2") SDW("%2", "%3") SDW("%3", "%4") SDW("%4", "%5") SDW("%5", "%6") SDW("%6", "%7") SDW("%7", "%0"))
+    }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   if ((threadIdx.x & 63) == 0) out[blockIdx.x * 4 + threadIdx.x / 64] = t1 - t0;
@@ -56,7 +72,9 @@ __global__ __launch_bounds__(256) void k_rate(uint32_t iters, uint64_t* out, uin
 static const char* kNames[] = {"v_add_u32", "v_xor_b32", "v_bfrev_b32", "v_ffbh_u32", "v_bfe_u32",
                                "v_alignbit_b32", "v_lshl_or_b32", "v_mul_f32", "v_cvt_i32_f32", "v_max3_u32",
                                "v_cndmask_b32", "v_lshl/rrev_b64", "v_bitop3_b32", "v_lshlrev_b32", "v_add3_u32",
-                               "v_perm_b32"};
+                               "v_perm_b32", "v_cndmask_e64 sgpr", "v_sub_u32", "v_ashrrev_i32", "v_and_or_b32",
+                               "v_or3_b32", "v_and_b32", "v_or_b32", "v_min_u32", "v_lshrrev_b32", "v_max3_f32",
+                               "v_lshlrev_b32_sdwa"};
 
 template <int OP>
 static void run(int wg_per_cu, int ncu)
@@ -92,7 +110,9 @@ int main()
   for (int w : {1, 2, 8}) {
     run<0>(w, ncu); run<1>(w, ncu); run<2>(w, ncu); run<3>(w, ncu); run<4>(w, ncu); run<5>(w, ncu);
     run<6>(w, ncu); run<7>(w, ncu); run<8>(w, ncu); run<9>(w, ncu); run<10>(w, ncu); run<11>(w, ncu);
-    run<12>(w, ncu); run<13>(w, ncu); run<14>(w, ncu); run<15>(w, ncu);
+    run<12>(w, ncu); run<13>(w, ncu); run<14>(w, ncu); run<15>(w, ncu); run<16>(w, ncu); run<17>(w, ncu);
+    run<18>(w, ncu); run<19>(w, ncu); run<20>(w, ncu); run<21>(w, ncu); run<22>(w, ncu); run<23>(w, ncu);
+    run<24>(w, ncu); run<25>(w, ncu); run<26>(w, ncu);
   }
   return 0;
 }
