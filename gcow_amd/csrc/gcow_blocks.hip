@@ -1,0 +1,241 @@
+// gcow_blocks.hip -- the 2-D / 3-D block kernels (one block per lane): tiles encoder instantiations, fixed-rate 3-D
+// encoder / decoder, the generic and LDS-staged decoders, and their launchers. A translation unit of its own so the
+// heavy 64-coefficient instantiations compile in parallel with gcow_kernels.hip.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "codec_device.h"
+#include "kernels.h"
+#include "tiles.h"
+
+namespace gcow {
+
+// ------------------------------------------------------------------------------------------------ 3-D fixed rate
+// Fixed-rate 3-D blocks whose budget is a whole number of 32-bit words (maxbits = 32 WPB; rates 1, 2, 4, 8, 16, 32):
+// one block per lane, 256 consecutive blocks per workgroup. The lane codes its block (generic 64-coefficient coder,
+// encode.c:457-495 with libzfp's 3-D transform and perm_3) into its own LDS words through LaneWordWriter -- whole
+// words, no atomics -- and the workgroup then stores its 256 WPB contiguous stream words coalesced.
+template <int DT, uint32_t WPB>
+__global__ __launch_bounds__(256) void k_encode3d_fixed(FieldDesc F, Params p, uint32_t* __restrict__ out32)
+{
+  extern __shared__ uint32_t lds_w[];  // 256 x (WPB + 1) words (odd stride: conflict-free per-lane words)
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * 256u;
+  const uint32_t nvalid = min(256u, F.nblocks - b0);
+  uint32_t* mine = lds_w + tid * (WPB + 1);
+  if (tid < nvalid) {
+    float f[64];
+    gather_block<3, DT>(F, b0 + tid, f);
+    LaneWordWriter w{mine, 0ull, 0u, 0u, WPB * 32u};
+    encode_block<3>(w, f, p);
+    w.finish(mine + WPB);
+  }
+  __syncthreads();
+  uint32_t* dst = out32 + (uint64_t)b0 * WPB;
+  for (uint32_t j = tid; j < nvalid * WPB; j += 256) dst[j] = lds_w[(j / WPB) * (WPB + 1) + (j % WPB)];
+  if (blockIdx.x == gridDim.x - 1 && tid == 0 && (((uint64_t)F.nblocks * WPB) & 1))
+    out32[(uint64_t)F.nblocks * WPB] = 0u;  // stream_flush: zero-pad to a 64-bit boundary
+}
+
+// The matching decoder: the workgroup stages its 256 blocks' stream words in LDS (coalesced), each lane decodes its
+// block from LDS (libzfp decode semantics) and scatters it.
+template <uint32_t WPB>
+__global__ __launch_bounds__(256) void k_decode3d_fixed(FieldDesc F, Params p, const uint32_t* __restrict__ in32)
+{
+  extern __shared__ uint32_t lds_w[];  // 256 x (WPB + 2) words: the block, then two zero pad words for peek64
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * 256u;
+  const uint32_t nvalid = min(256u, F.nblocks - b0);
+  const uint32_t* src = in32 + (uint64_t)b0 * WPB;
+  for (uint32_t j = tid; j < nvalid * WPB; j += 256) lds_w[(j / WPB) * (WPB + 2) + (j % WPB)] = src[j];
+  lds_w[tid * (WPB + 2) + WPB] = 0u;
+  lds_w[tid * (WPB + 2) + WPB + 1] = 0u;
+  __syncthreads();
+  if (tid < nvalid) {
+    WordBitReader r{lds_w + tid * (WPB + 2), 0};
+    float f[64];
+    decode_block<3>(r, p, f);
+    scatter_block<3>(F, b0 + tid, f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ decode
+template <int D>
+__global__ __launch_bounds__(64) void k_decode(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                               const uint64_t* __restrict__ index, uint32_t chunk, uint64_t nchunks,
+                                               uint32_t fixed, uint64_t base_bits, uint64_t* __restrict__ end_out)
+{
+  constexpr int B = Dim<D>::B;
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  BitReader r{in, 0};
+  uint64_t b = c * chunk;
+  const uint64_t bend = min<uint64_t>(b + chunk, F.nblocks);
+  r.pos = base_bits + (fixed ? b * p.maxbits : (index ? index[c] : 0ull));
+  for (; b < bend; b++) {
+    float f[B];
+    decode_block<D>(r, p, f);
+    scatter_block<D>(F, (uint32_t)b, f);
+  }
+  if (end_out && c == nchunks - 1) *end_out = r.pos;
+}
+
+// One block per lane with the workgroup's stream span staged in LDS (coalesced copy) and read through
+// WordBitReader: blocks start at the block index (stride 1) or at b * maxbits (fixed rate). A span above the
+// capacity (1024 bits per block on average) decodes from global memory.
+template <int D>
+__global__ __launch_bounds__(64) void k_decode_staged(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                      uint64_t in_words, const uint64_t* __restrict__ index,
+                                                      uint32_t fixed, uint64_t base_bits,
+                                                      uint64_t* __restrict__ end_out)
+{
+  constexpr int B = Dim<D>::B;
+  constexpr uint32_t CAPW = 64 * 1024 / 32;  // 32-bit words
+  __shared__ uint32_t sw[CAPW + 4];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * 64, nb = F.nblocks;
+  auto start_of = [&](uint64_t b) { return base_bits + (fixed ? b * p.maxbits : index[b]); };
+  const uint64_t s0 = start_of(b0);
+  const uint64_t w0 = s0 >> 5;  // 32-bit word index
+  const uint64_t in_w32 = 2 * in_words;
+  const uint64_t wend = b0 + 64 < nb ? (start_of(b0 + 64) + 31) >> 5 : in_w32;
+  const uint64_t span = min<uint64_t>(wend, in_w32) - w0;
+  const bool staged = span <= CAPW;
+  const uint32_t* in32 = (const uint32_t*)in;
+  if (staged)
+    for (uint32_t j = tid; j < (uint32_t)span + 4; j += 64) sw[j] = w0 + j < in_w32 ? in32[w0 + j] : 0u;
+  __syncthreads();
+  const uint64_t b = b0 + tid;
+  if (b >= nb) return;
+  float f[B];
+  uint64_t end;
+  if (staged) {
+    WordBitReader r{sw, start_of(b) - 32 * w0};
+    decode_block<D>(r, p, f);
+    end = r.pos + 32 * w0;
+  } else {
+    BitReader r{in, start_of(b)};
+    decode_block<D>(r, p, f);
+    end = r.pos;
+  }
+  scatter_block<D>(F, (uint32_t)b, f);
+  if (end_out && b == nb - 1) *end_out = end;
+}
+
+// ------------------------------------------------------------------------------------------------ launchers
+static inline hipStream_t S(void* s) { return (hipStream_t)s; }
+
+template <int D, int DT, uint32_t T>
+static hipError_t launch_tiles23_t(const FieldDesc& F, const Params& p, const TilePlan& plan, uint32_t* out32,
+                                   uint64_t* ws_sums, uint64_t* ws_base, uint64_t* d_total, uint64_t* index,
+                                   uint32_t index_shift, const uint64_t* d_base, hipStream_t st)
+{
+  const size_t lds = (size_t)plan.lds_words * 4;
+  if (plan.fixed) {
+    auto kern = k_encode_tiles<D, DT, T, true>;
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    kern<<<plan.nranges, T, lds, st>>>(F, p, plan.range, nullptr, out32, index, index_shift);
+    return hipGetLastError();
+  }
+  k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
+  hipError_t e = launch_scan_ranges(ws_sums, plan.nranges, ws_base, d_total, out32, d_base, st);
+  if (e != hipSuccess) return e;
+  auto kern = k_encode_tiles<D, DT, T, false>;
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  kern<<<plan.nranges, T, lds, st>>>(F, p, plan.range, ws_base, out32, index, index_shift);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode_tiles23(const FieldDesc& F, const Params& p, const TilePlan& plan, uint32_t* out32,
+                                 uint64_t* ws_sums, uint64_t* ws_base, uint64_t* d_total, uint64_t* index,
+                                 uint32_t index_shift, const uint64_t* d_base, void* stream)
+{
+  hipStream_t st = S(stream);
+  const bool bf = F.dtype == DT_BF16;
+#define GCOW_TILES(D, T)                                                                                          \
+  return bf ? launch_tiles23_t<D, DT_BF16, T>(F, p, plan, out32, ws_sums, ws_base, d_total, index, index_shift, d_base, st) \
+            : launch_tiles23_t<D, DT_F32, T>(F, p, plan, out32, ws_sums, ws_base, d_total, index, index_shift, d_base, st)
+  if (F.dims == 2) {
+    if (plan.threads == 256) { GCOW_TILES(2, 256); } else { GCOW_TILES(2, 64); }
+  }
+  GCOW_TILES(3, 64);
+#undef GCOW_TILES
+}
+
+hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
+                         uint32_t chunk, uint64_t nchunks, bool fixed, uint64_t base_bits, uint64_t* end_out,
+                         void* stream, uint64_t in_words)
+{
+  if (chunk == 1 && in_words && (fixed || index) && F.dims >= 2) {
+    const uint32_t g = (uint32_t)((F.nblocks + 63) / 64);
+    if (F.dims == 2) k_decode_staged<2><<<g, 64, 0, S(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
+    else k_decode_staged<3><<<g, 64, 0, S(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
+    return hipGetLastError();
+  }
+  const uint32_t T = 64;
+  const uint64_t grid = (nchunks + T - 1) / T;
+  if (!grid) return hipSuccess;
+  if (F.dims == 1) k_decode<1><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
+  else if (F.dims == 2) k_decode<2><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
+  else k_decode<3><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
+  return hipGetLastError();
+}
+
+template <int DT, uint32_t WPB>
+static hipError_t launch_enc3d_t(const FieldDesc& F, const Params& p, uint32_t* out32, hipStream_t st)
+{
+  const size_t lds = 256 * (WPB + 1) * 4;
+  auto kern = k_encode3d_fixed<DT, WPB>;
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  kern<<<(F.nblocks + 255) / 256, 256, lds, st>>>(F, p, out32);
+  return hipGetLastError();
+}
+
+template <uint32_t WPB>
+static hipError_t launch_dec3d_t(const FieldDesc& F, const Params& p, const uint32_t* in32, hipStream_t st)
+{
+  const size_t lds = 256 * (WPB + 2) * 4;
+  auto kern = k_decode3d_fixed<WPB>;
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  kern<<<(F.nblocks + 255) / 256, 256, lds, st>>>(F, p, in32);
+  return hipGetLastError();
+}
+
+bool fixed3d_ok(uint32_t maxbits)
+{
+  const uint32_t w = maxbits / 32;
+  return maxbits % 32 == 0 && (w == 2 || w == 4 || w == 8 || w == 16 || w == 32 || w == 64);
+}
+
+hipError_t launch_encode3d_fixed(const FieldDesc& F, const Params& p, uint32_t* out32, void* stream)
+{
+  hipStream_t st = S(stream);
+  const bool bf = F.dtype == DT_BF16;
+#define GCOW_E3(W) return bf ? launch_enc3d_t<DT_BF16, W>(F, p, out32, st) : launch_enc3d_t<DT_F32, W>(F, p, out32, st)
+  switch (p.maxbits / 32) {
+    case 2: GCOW_E3(2);
+    case 4: GCOW_E3(4);
+    case 8: GCOW_E3(8);
+    case 16: GCOW_E3(16);
+    case 32: GCOW_E3(32);
+    case 64: GCOW_E3(64);
+  }
+#undef GCOW_E3
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_decode3d_fixed(const FieldDesc& F, const Params& p, const uint32_t* in32, void* stream)
+{
+  hipStream_t st = S(stream);
+  switch (p.maxbits / 32) {
+    case 2: return launch_dec3d_t<2>(F, p, in32, st);
+    case 4: return launch_dec3d_t<4>(F, p, in32, st);
+    case 8: return launch_dec3d_t<8>(F, p, in32, st);
+    case 16: return launch_dec3d_t<16>(F, p, in32, st);
+    case 32: return launch_dec3d_t<32>(F, p, in32, st);
+    case 64: return launch_dec3d_t<64>(F, p, in32, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace gcow

@@ -20,129 +20,9 @@
 
 #include "codec_device.h"
 #include "kernels.h"
+#include "tiles.h"
 
 namespace gcow {
-
-// ------------------------------------------------------------------------------------------------ gather
-__device__ __forceinline__ uint32_t pad_index(uint32_t i, uint32_t nv)
-{
-  // pad_partial_block fall-through (sw/src/encode.c:41-60): 1 -> v0 v0 v0 v0, 2 -> v0 v1 v1 v0, 3 -> v0 v1 v2 v0
-  return nv >= 4 ? i : (nv == 1 ? 0u : (i == 3 ? 0u : (nv == 2 && i == 2 ? 1u : i)));
-}
-
-template <int DT>
-__device__ __forceinline__ float load_elem(const void* base, int64_t off)
-{
-  if constexpr (DT == DT_BF16) {
-    uint32_t h = ((const uint16_t*)base)[off];
-    return __uint_as_float(h << 16);  // exact bf16 -> fp32 widening
-  } else {
-    return ((const float*)base)[off];
-  }
-}
-
-// Load 4 consecutive values starting at element offset off (16-B aligned for f32, 8-B for bf16 when vec).
-template <int DT>
-__device__ __forceinline__ void load_row4(const void* base, int64_t off, float* f)
-{
-  if constexpr (DT == DT_BF16) {
-    uint2 v = *(const uint2*)((const uint16_t*)base + off);
-    f[0] = __uint_as_float(v.x << 16);
-    f[1] = __uint_as_float(v.x & 0xffff0000u);
-    f[2] = __uint_as_float(v.y << 16);
-    f[3] = __uint_as_float(v.y & 0xffff0000u);
-  } else {
-    float4 v = *(const float4*)((const float*)base + off);
-    f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
-  }
-}
-
-// gather_2d_block / gather_partial_2d_block / gather_partial_4d_block (sw/src/encode.c:62-126), generic d.
-template <int D, int DT>
-__device__ __forceinline__ void gather_block(const FieldDesc& F, uint32_t b, float* f)
-{
-  uint32_t ix, iy = 0, iz = 0;
-  if constexpr (D == 1) {
-    ix = b;
-  } else if constexpr (D == 2) {
-    iy = b / F.bx;
-    ix = b - iy * F.bx;
-  } else {
-    uint32_t r = b / F.bx;
-    ix = b - r * F.bx;
-    iz = r / F.by;
-    iy = r - iz * F.by;
-  }
-  const uint64_t x0 = 4ull * ix, y0 = 4ull * iy, z0 = 4ull * iz;
-  const uint32_t nvx = (uint32_t)min<uint64_t>(4, F.n[0] - x0);
-  const uint32_t nvy = D > 1 ? (uint32_t)min<uint64_t>(4, F.n[1] - y0) : 1u;
-  const uint32_t nvz = D > 2 ? (uint32_t)min<uint64_t>(4, F.n[2] - z0) : 1u;
-  const int64_t base = (int64_t)x0 * F.s[0] + (int64_t)y0 * F.s[1] + (int64_t)z0 * F.s[2];
-  const bool full = nvx == 4 && (D < 2 || nvy == 4) && (D < 3 || nvz == 4);
-  if (full && F.vec) {
-#pragma unroll
-    for (int z = 0; z < (D > 2 ? 4 : 1); z++)
-#pragma unroll
-      for (int y = 0; y < (D > 1 ? 4 : 1); y++)
-        load_row4<DT>(F.data, base + (int64_t)y * F.s[1] + (int64_t)z * F.s[2], f + 16 * z + 4 * y);
-  } else {
-#pragma unroll
-    for (int z = 0; z < (D > 2 ? 4 : 1); z++)
-#pragma unroll
-      for (int y = 0; y < (D > 1 ? 4 : 1); y++)
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-          int64_t off = (int64_t)pad_index(x, nvx) * F.s[0];
-          if (D > 1) off += (int64_t)pad_index(y, nvy) * F.s[1];
-          if (D > 2) off += (int64_t)pad_index(z, nvz) * F.s[2];
-          f[16 * z + 4 * y + x] = load_elem<DT>(F.data, base + off);
-        }
-  }
-}
-
-// scatter_2d_block / scatter_partial_2d_block (sw/src/decode.c:27-42), generic d, fp32 output.
-template <int D>
-__device__ __forceinline__ void scatter_block(const FieldDesc& F, uint32_t b, const float* f)
-{
-  uint32_t ix, iy = 0, iz = 0;
-  if constexpr (D == 1) {
-    ix = b;
-  } else if constexpr (D == 2) {
-    iy = b / F.bx;
-    ix = b - iy * F.bx;
-  } else {
-    uint32_t r = b / F.bx;
-    ix = b - r * F.bx;
-    iz = r / F.by;
-    iy = r - iz * F.by;
-  }
-  const uint64_t x0 = 4ull * ix, y0 = 4ull * iy, z0 = 4ull * iz;
-  const uint32_t nvx = (uint32_t)min<uint64_t>(4, F.n[0] - x0);
-  const uint32_t nvy = D > 1 ? (uint32_t)min<uint64_t>(4, F.n[1] - y0) : 1u;
-  const uint32_t nvz = D > 2 ? (uint32_t)min<uint64_t>(4, F.n[2] - z0) : 1u;
-  float* out = (float*)F.data;
-  const int64_t base = (int64_t)x0 * F.s[0] + (int64_t)y0 * F.s[1] + (int64_t)z0 * F.s[2];
-  const bool full = nvx == 4 && (D < 2 || nvy == 4) && (D < 3 || nvz == 4);
-  if (full && F.vec) {
-#pragma unroll
-    for (int z = 0; z < (D > 2 ? 4 : 1); z++)
-#pragma unroll
-      for (int y = 0; y < (D > 1 ? 4 : 1); y++) {
-        const float* g = f + 16 * z + 4 * y;
-        *(float4*)(out + base + (int64_t)y * F.s[1] + (int64_t)z * F.s[2]) = make_float4(g[0], g[1], g[2], g[3]);
-      }
-  } else {
-    // static trip counts with guards: a dynamically indexed f[] would live in scratch
-#pragma unroll
-    for (uint32_t z = 0; z < (D > 2 ? 4u : 1u); z++)
-#pragma unroll
-      for (uint32_t y = 0; y < (D > 1 ? 4u : 1u); y++)
-#pragma unroll
-        for (uint32_t x = 0; x < 4u; x++)
-          if (x < nvx && y < nvy && z < nvz)
-            out[base + (int64_t)x * F.s[0] + (int64_t)y * F.s[1] + (int64_t)z * F.s[2]] = f[16 * z + 4 * y + x];
-  }
-}
 
 // ------------------------------------------------------------------------------------------------ 1-D fast path
 // Plane-code table for 4-value blocks: entry (n, x) = verbatim n bits of plane x followed by the group-test code of
@@ -739,61 +619,6 @@ __global__ void k_encode_fixed1d_tail(const void* __restrict__ in, uint64_t nval
   else ((uint32_t*)out)[b] = (uint32_t)w;
 }
 
-// ------------------------------------------------------------------------------------------------ tiles
-template <uint32_t T>
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* total, uint32_t* sh)
-{
-  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= (uint32_t)o) x += y;
-  }
-  if (T > 64) {
-    if (lane == 63) sh[wid] = x;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < T / 64; w++) {
-      uint32_t s = sh[w];
-      off += w < wid ? s : 0u;
-      tot += s;
-    }
-    __syncthreads();
-    *total = tot;
-    return off + x - v;
-  } else {
-    *total = __shfl(x, 63, 64);
-    return x - v;
-  }
-}
-
-// Pass 1: sum of block bit lengths per contiguous range of `range` blocks.
-template <int D, int DT, uint32_t T>
-__global__ __launch_bounds__(T) void k_count(FieldDesc F, Params p, uint32_t range, uint64_t* __restrict__ sums)
-{
-  constexpr int B = Dim<D>::B;
-  __shared__ uint64_t red[T / 64];
-  const uint64_t b0 = (uint64_t)blockIdx.x * range;
-  const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
-  uint64_t acc = 0;
-  for (uint64_t b = b0 + threadIdx.x; b < b1; b += T) {
-    float f[B];
-    gather_block<D, DT>(F, (uint32_t)b, f);
-    acc += count_block<D>(f, p);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t s = 0;
-    for (uint32_t i = 0; i < T / 64; i++) s += red[i];
-    sums[blockIdx.x] = s;
-  }
-}
-
 // Exclusive scan of the range totals (one workgroup). base[] gets nranges + 1 entries (last = total bits); the
 // 32-bit words two ranges share are zeroed so both sides can atomicOr into them; the stream's flush word too.
 // d_base (optional): the stream already holds *d_base bits (chunked / appended encode); every offset starts there and
@@ -827,71 +652,6 @@ __global__ __launch_bounds__(1024) void k_scan_ranges(const uint64_t* __restrict
     const uint64_t tot = b0 + part[1023];
     base[nranges] = tot;
     if (total) *total = tot;
-  }
-}
-
-// Pass 2 / generic fixed rate: each workgroup encodes blocks [range*wg, range*(wg+1)) tile by tile.
-template <int D, int DT, uint32_t T, bool FIXED>
-__global__ __launch_bounds__(T) void k_encode_tiles(FieldDesc F, Params p, uint32_t range,
-                                                    const uint64_t* __restrict__ rbase, uint32_t* __restrict__ out32,
-                                                    uint64_t* __restrict__ index, uint32_t index_shift)
-{
-  constexpr int B = Dim<D>::B;
-  extern __shared__ uint32_t lds[];
-  __shared__ uint32_t scan_sh[T / 64 > 0 ? T / 64 : 1];
-  const uint32_t tid = threadIdx.x;
-  const uint64_t b0 = (uint64_t)blockIdx.x * range;
-  const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
-  const bool final_range = b1 == F.nblocks;
-  uint64_t base = FIXED ? b0 * p.maxbits : rbase[blockIdx.x];
-  const uint64_t first_word = base >> 5;
-  const bool first_shared = (base & 31) != 0;
-  uint32_t carry = 0;
-  for (uint64_t t0 = b0; t0 < b1; t0 += T) {
-    const uint64_t b = t0 + tid;
-    const bool valid = b < b1;
-    float f[B];
-    uint32_t len = 0;
-    if (valid) {
-      gather_block<D, DT>(F, (uint32_t)b, f);
-      if (FIXED) {
-        len = p.maxbits;
-      } else {
-        len = count_block<D>(f, p);
-      }
-    }
-    uint32_t tile_total;
-    const uint32_t excl = block_exclusive_scan<T>(len, &tile_total, scan_sh);
-    const uint32_t lbase = (uint32_t)(base & 31);
-    const uint32_t end_local = lbase + tile_total;
-    const uint32_t W = (end_local + 31) >> 5;
-    for (uint32_t j = tid; j < W; j += T) lds[j] = (j == 0) ? carry : 0u;
-    __syncthreads();
-    if (valid) {
-      LdsWriter w{lds, lbase + excl, lbase + excl + len};
-      encode_block<D>(w, f, p);
-      if (index && ((b & ((1ull << index_shift) - 1)) == 0)) index[b >> index_shift] = base + excl;
-    }
-    __syncthreads();
-    const bool last_tile = t0 + T >= b1;
-    const bool partial = (end_local & 31) != 0;
-    const uint32_t Wstore = (last_tile || !partial) ? W : (end_local >> 5);
-    const uint64_t gw0 = base >> 5;
-    for (uint32_t j = tid; j < Wstore; j += T) {
-      const uint64_t gw = gw0 + j;
-      const uint32_t v = lds[j];
-      const bool shared = (gw == first_word && first_shared) || (last_tile && partial && !final_range && j == W - 1);
-      if (shared) atomicOr(out32 + gw, v);
-      else out32[gw] = v;
-    }
-    if (last_tile && final_range && tid == 0) {
-      // stream_flush: zero-pad to a 64-bit boundary
-      const uint64_t endw = (base + tile_total + 31) >> 5;
-      if (endw & 1) out32[endw] = 0u;
-    }
-    carry = (!last_tile && partial) ? lds[end_local >> 5] : 0u;
-    base += tile_total;
-    __syncthreads();
   }
 }
 
@@ -1266,55 +1026,6 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
   }
 }
 
-// ------------------------------------------------------------------------------------------------ 3-D fixed rate
-// Fixed-rate 3-D blocks whose budget is a whole number of 32-bit words (maxbits = 32 WPB; rates 1, 2, 4, 8, 16, 32):
-// one block per lane, 256 consecutive blocks per workgroup. The lane codes its block (generic 64-coefficient coder,
-// encode.c:457-495 with libzfp's 3-D transform and perm_3) into its own LDS words through LaneWordWriter -- whole
-// words, no atomics -- and the workgroup then stores its 256 WPB contiguous stream words coalesced.
-template <int DT, uint32_t WPB>
-__global__ __launch_bounds__(256) void k_encode3d_fixed(FieldDesc F, Params p, uint32_t* __restrict__ out32)
-{
-  extern __shared__ uint32_t lds_w[];  // 256 x (WPB + 1) words (odd stride: conflict-free per-lane words)
-  const uint32_t tid = threadIdx.x;
-  const uint32_t b0 = blockIdx.x * 256u;
-  const uint32_t nvalid = min(256u, F.nblocks - b0);
-  uint32_t* mine = lds_w + tid * (WPB + 1);
-  if (tid < nvalid) {
-    float f[64];
-    gather_block<3, DT>(F, b0 + tid, f);
-    LaneWordWriter w{mine, 0ull, 0u, 0u, WPB * 32u};
-    encode_block<3>(w, f, p);
-    w.finish(mine + WPB);
-  }
-  __syncthreads();
-  uint32_t* dst = out32 + (uint64_t)b0 * WPB;
-  for (uint32_t j = tid; j < nvalid * WPB; j += 256) dst[j] = lds_w[(j / WPB) * (WPB + 1) + (j % WPB)];
-  if (blockIdx.x == gridDim.x - 1 && tid == 0 && (((uint64_t)F.nblocks * WPB) & 1))
-    out32[(uint64_t)F.nblocks * WPB] = 0u;  // stream_flush: zero-pad to a 64-bit boundary
-}
-
-// The matching decoder: the workgroup stages its 256 blocks' stream words in LDS (coalesced), each lane decodes its
-// block from LDS (libzfp decode semantics) and scatters it.
-template <uint32_t WPB>
-__global__ __launch_bounds__(256) void k_decode3d_fixed(FieldDesc F, Params p, const uint32_t* __restrict__ in32)
-{
-  extern __shared__ uint32_t lds_w[];  // 256 x (WPB + 2) words: the block, then two zero pad words for peek64
-  const uint32_t tid = threadIdx.x;
-  const uint32_t b0 = blockIdx.x * 256u;
-  const uint32_t nvalid = min(256u, F.nblocks - b0);
-  const uint32_t* src = in32 + (uint64_t)b0 * WPB;
-  for (uint32_t j = tid; j < nvalid * WPB; j += 256) lds_w[(j / WPB) * (WPB + 2) + (j % WPB)] = src[j];
-  lds_w[tid * (WPB + 2) + WPB] = 0u;
-  lds_w[tid * (WPB + 2) + WPB + 1] = 0u;
-  __syncthreads();
-  if (tid < nvalid) {
-    WordBitReader r{lds_w + tid * (WPB + 2), 0};
-    float f[64];
-    decode_block<3>(r, p, f);
-    scatter_block<3>(F, b0 + tid, f);
-  }
-}
-
 // ------------------------------------------------------------------------------------------------ 4-D blocks
 // sw/ declares the 4-D gather (gather_partial_4d_block, sw/src/encode.c:90-126) and zfp_input's
 // nw / sw (sw/include/types.h:51-56) but never codes 4-D; libzfp 0.5.5 does, with perm_4 and x, y, z, w lifts.
@@ -1625,69 +1336,6 @@ __global__ void k_widen_u32(const uint32_t* __restrict__ a, uint32_t n, uint64_t
 {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i < n) o[i] = a[i];
-}
-
-// ------------------------------------------------------------------------------------------------ decode
-template <int D>
-__global__ __launch_bounds__(64) void k_decode(FieldDesc F, Params p, const uint64_t* __restrict__ in,
-                                               const uint64_t* __restrict__ index, uint32_t chunk, uint64_t nchunks,
-                                               uint32_t fixed, uint64_t base_bits, uint64_t* __restrict__ end_out)
-{
-  constexpr int B = Dim<D>::B;
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nchunks) return;
-  BitReader r{in, 0};
-  uint64_t b = c * chunk;
-  const uint64_t bend = min<uint64_t>(b + chunk, F.nblocks);
-  r.pos = base_bits + (fixed ? b * p.maxbits : (index ? index[c] : 0ull));
-  for (; b < bend; b++) {
-    float f[B];
-    decode_block<D>(r, p, f);
-    scatter_block<D>(F, (uint32_t)b, f);
-  }
-  if (end_out && c == nchunks - 1) *end_out = r.pos;
-}
-
-// One block per lane with the workgroup's stream span staged in LDS (coalesced copy) and read through
-// WordBitReader: blocks start at the block index (stride 1) or at b * maxbits (fixed rate). A span above the
-// capacity (1024 bits per block on average) decodes from global memory.
-template <int D>
-__global__ __launch_bounds__(64) void k_decode_staged(FieldDesc F, Params p, const uint64_t* __restrict__ in,
-                                                      uint64_t in_words, const uint64_t* __restrict__ index,
-                                                      uint32_t fixed, uint64_t base_bits,
-                                                      uint64_t* __restrict__ end_out)
-{
-  constexpr int B = Dim<D>::B;
-  constexpr uint32_t CAPW = 64 * 1024 / 32;  // 32-bit words
-  __shared__ uint32_t sw[CAPW + 4];
-  const uint32_t tid = threadIdx.x;
-  const uint64_t b0 = (uint64_t)blockIdx.x * 64, nb = F.nblocks;
-  auto start_of = [&](uint64_t b) { return base_bits + (fixed ? b * p.maxbits : index[b]); };
-  const uint64_t s0 = start_of(b0);
-  const uint64_t w0 = s0 >> 5;  // 32-bit word index
-  const uint64_t in_w32 = 2 * in_words;
-  const uint64_t wend = b0 + 64 < nb ? (start_of(b0 + 64) + 31) >> 5 : in_w32;
-  const uint64_t span = min<uint64_t>(wend, in_w32) - w0;
-  const bool staged = span <= CAPW;
-  const uint32_t* in32 = (const uint32_t*)in;
-  if (staged)
-    for (uint32_t j = tid; j < (uint32_t)span + 4; j += 64) sw[j] = w0 + j < in_w32 ? in32[w0 + j] : 0u;
-  __syncthreads();
-  const uint64_t b = b0 + tid;
-  if (b >= nb) return;
-  float f[B];
-  uint64_t end;
-  if (staged) {
-    WordBitReader r{sw, start_of(b) - 32 * w0};
-    decode_block<D>(r, p, f);
-    end = r.pos + 32 * w0;
-  } else {
-    BitReader r{in, start_of(b)};
-    decode_block<D>(r, p, f);
-    end = r.pos;
-  }
-  scatter_block<D>(F, (uint32_t)b, f);
-  if (end_out && b == nb - 1) *end_out = end;
 }
 
 // ------------------------------------------------------------------------------------------------ fast 1-D decode
@@ -2471,90 +2119,9 @@ hipError_t launch_encode_tiles(const FieldDesc& F, const Params& p, const TilePl
 #define GCOW_TILES(D, T)                                                                                       \
   return bf ? launch_tiles_t<D, DT_BF16, T>(F, p, plan, out32, ws_sums, ws_base, d_total, index, index_shift, d_base, st) \
             : launch_tiles_t<D, DT_F32, T>(F, p, plan, out32, ws_sums, ws_base, d_total, index, index_shift, d_base, st)
-  if (F.dims == 1) {
-    if (plan.threads == 256) { GCOW_TILES(1, 256); } else { GCOW_TILES(1, 64); }
-  } else if (F.dims == 2) {
-    if (plan.threads == 256) { GCOW_TILES(2, 256); } else { GCOW_TILES(2, 64); }
-  } else {
-    GCOW_TILES(3, 64);
-  }
+  if (F.dims != 1) return launch_encode_tiles23(F, p, plan, out32, ws_sums, ws_base, d_total, index, index_shift, d_base, st);
+  if (plan.threads == 256) { GCOW_TILES(1, 256); } else { GCOW_TILES(1, 64); }
 #undef GCOW_TILES
-}
-
-hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in, const uint64_t* index,
-                         uint32_t chunk, uint64_t nchunks, bool fixed, uint64_t base_bits, uint64_t* end_out,
-                         void* stream, uint64_t in_words)
-{
-  if (chunk == 1 && in_words && (fixed || index) && F.dims >= 2) {
-    const uint32_t g = (uint32_t)((F.nblocks + 63) / 64);
-    if (F.dims == 2) k_decode_staged<2><<<g, 64, 0, S(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
-    else k_decode_staged<3><<<g, 64, 0, S(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
-    return hipGetLastError();
-  }
-  const uint32_t T = 64;
-  const uint64_t grid = (nchunks + T - 1) / T;
-  if (!grid) return hipSuccess;
-  if (F.dims == 1) k_decode<1><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
-  else if (F.dims == 2) k_decode<2><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
-  else k_decode<3><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
-  return hipGetLastError();
-}
-
-template <int DT, uint32_t WPB>
-static hipError_t launch_enc3d_t(const FieldDesc& F, const Params& p, uint32_t* out32, hipStream_t st)
-{
-  const size_t lds = 256 * (WPB + 1) * 4;
-  auto kern = k_encode3d_fixed<DT, WPB>;
-  if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  kern<<<(F.nblocks + 255) / 256, 256, lds, st>>>(F, p, out32);
-  return hipGetLastError();
-}
-
-template <uint32_t WPB>
-static hipError_t launch_dec3d_t(const FieldDesc& F, const Params& p, const uint32_t* in32, hipStream_t st)
-{
-  const size_t lds = 256 * (WPB + 2) * 4;
-  auto kern = k_decode3d_fixed<WPB>;
-  if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  kern<<<(F.nblocks + 255) / 256, 256, lds, st>>>(F, p, in32);
-  return hipGetLastError();
-}
-
-bool fixed3d_ok(uint32_t maxbits)
-{
-  const uint32_t w = maxbits / 32;
-  return maxbits % 32 == 0 && (w == 2 || w == 4 || w == 8 || w == 16 || w == 32 || w == 64);
-}
-
-hipError_t launch_encode3d_fixed(const FieldDesc& F, const Params& p, uint32_t* out32, void* stream)
-{
-  hipStream_t st = S(stream);
-  const bool bf = F.dtype == DT_BF16;
-#define GCOW_E3(W) return bf ? launch_enc3d_t<DT_BF16, W>(F, p, out32, st) : launch_enc3d_t<DT_F32, W>(F, p, out32, st)
-  switch (p.maxbits / 32) {
-    case 2: GCOW_E3(2);
-    case 4: GCOW_E3(4);
-    case 8: GCOW_E3(8);
-    case 16: GCOW_E3(16);
-    case 32: GCOW_E3(32);
-    case 64: GCOW_E3(64);
-  }
-#undef GCOW_E3
-  return hipErrorInvalidValue;
-}
-
-hipError_t launch_decode3d_fixed(const FieldDesc& F, const Params& p, const uint32_t* in32, void* stream)
-{
-  hipStream_t st = S(stream);
-  switch (p.maxbits / 32) {
-    case 2: return launch_dec3d_t<2>(F, p, in32, st);
-    case 4: return launch_dec3d_t<4>(F, p, in32, st);
-    case 8: return launch_dec3d_t<8>(F, p, in32, st);
-    case 16: return launch_dec3d_t<16>(F, p, in32, st);
-    case 32: return launch_dec3d_t<32>(F, p, in32, st);
-    case 64: return launch_dec3d_t<64>(F, p, in32, st);
-  }
-  return hipErrorInvalidValue;
 }
 
 hipError_t launch_encode4d(const FieldDesc& F, const Params& p, uint32_t* lens, const uint64_t* rbase, uint32_t* out32,
@@ -2616,6 +2183,13 @@ hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint
     else k_decode_fixed1d_np<32, 16><<<(nc + 4095) / 4096, 256, 0, S(stream)>>>(in, nc, p, out, bb);
   }
   if (F.n[0] % 4) k_decode_tail1d<<<1, 1, 0, S(stream)>>>(F, p, in, base_bits, nfull);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* base, uint64_t* total, uint32_t* out32,
+                              const uint64_t* d_base, void* stream)
+{
+  k_scan_ranges<<<1, 1024, 0, S(stream)>>>(sums, nranges, base, total, out32, d_base);
   return hipGetLastError();
 }
 

@@ -60,6 +60,12 @@ hipError_t launch_decode4d_seq(const FieldDesc& F, const Params& p, const uint64
                                uint64_t* end, void* stream);
 hipError_t launch_scan_blocks(const uint32_t* lens, uint32_t nblocks, uint64_t* sums, uint64_t* base, uint64_t* total,
                               uint32_t* out32, void* stream);
+// 2-D / 3-D tiles (gcow_blocks.hip); launch_encode_tiles forwards d >= 2 here
+hipError_t launch_encode_tiles23(const FieldDesc& F, const Params& p, const TilePlan& plan, uint32_t* out32,
+                                 uint64_t* ws_sums, uint64_t* ws_base, uint64_t* d_total, uint64_t* index,
+                                 uint32_t index_shift, const uint64_t* d_base, void* stream);
+hipError_t launch_scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* base, uint64_t* total, uint32_t* out32,
+                              const uint64_t* d_base, void* stream);
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
 hipError_t launch_prepend_header(uint64_t* dst, uint32_t off, const uint64_t* src, const uint64_t* d_bits,
                                  const uint64_t* header, uint64_t max_words, uint64_t* d_total, void* stream);
