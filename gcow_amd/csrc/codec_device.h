@@ -221,6 +221,28 @@ __device__ __forceinline__ void transpose32_stage(uint32_t* a)
   }
 }
 
+// The same transpose with every stage's results pinned in registers before the next stage starts: keeps the
+// scheduler from interleaving the stages of two 32-word transposes (which needs ~100 extra VGPRs).
+__device__ __forceinline__ void pin32(uint32_t* a)
+{
+#pragma unroll
+  for (int i = 0; i < 32; i++) asm volatile("" : "+v"(a[i]));
+}
+
+__device__ __forceinline__ void transpose32_pinned(uint32_t* a)
+{
+  transpose32_stage<16, 0x0000FFFFu>(a);
+  pin32(a);
+  transpose32_stage<8, 0x00FF00FFu>(a);
+  pin32(a);
+  transpose32_stage<4, 0x0F0F0F0Fu>(a);
+  pin32(a);
+  transpose32_stage<2, 0x33333333u>(a);
+  pin32(a);
+  transpose32_stage<1, 0x55555555u>(a);
+  pin32(a);
+}
+
 __device__ __forceinline__ void transpose32(uint32_t* a)
 {
   transpose32_stage<16, 0x0000FFFFu>(a);
@@ -390,14 +412,156 @@ __device__ __forceinline__ uint32_t encode_ints(W& w, const uint32_t* u, uint32_
   return bits < budget ? bits : budget;
 }
 
+// ---- the 64-coefficient coder, plane at a time without a loop over one-bits (3-D blocks)
+// Plane k of encode.c:279-339 with n coefficients already significant and r = x >> n is
+//   x[0 .. n-1] verbatim, then the group flag (r != 0), then -- if r != 0 -- E(r) through the last one-bit hb of r
+//   and a closing '0',
+// where E(r) writes every zero bit of r as '0' and every one-bit as '11' (the one-bit, then the flag that opens the
+// next group); the last one-bit's second '1' is that closing '0' instead. When the last one-bit is coefficient 63
+// (n + hb + 1 = 64) its one is implied: the code stops before it and there is no closing '0'. So a plane is two
+// appends: n + 1 verbatim/flag bits, and E(r) (hb + m + 1 bits with m = popcount(r), or hb + m - 1 at coefficient
+// 63) built from a 256-entry table of E over 8-bit chunks. Lanes do a fixed amount of work per plane; only chunks
+// past the wave's largest hb are skipped.
+struct DupTab {
+  uint32_t v[256];
+};
+
+__host__ __device__ constexpr DupTab make_dup_tab()
+{
+  DupTab T{};
+  for (uint32_t v = 0; v < 256; v++) {
+    uint32_t code = 0, len = 0;
+    for (uint32_t j = 0; j < 8; j++) {
+      if ((v >> j) & 1u) {
+        code |= 3u << len;
+        len += 2;
+      } else {
+        len += 1;
+      }
+    }
+    T.v[v] = code;
+  }
+  return T;
+}
+
+__device__ const DupTab g_dup_tab = make_dup_tab();
+
+// Lane-private run of zeroed LDS words with slack words after the block's budget: bits are OR-ed in at their
+// position (ds_or, no return), nothing is masked -- code past the budget lands in the slack, which is never stored.
+struct OrWriter {
+  uint32_t* w;
+  uint32_t pos;
+  __device__ __forceinline__ void put(uint64_t v, uint32_t n)
+  {
+    const uint32_t i = pos >> 5, sh = pos & 31u;
+    const uint64_t lo = v << sh;
+    const uint32_t hi = (uint32_t)((v >> 1) >> (63u - sh));  // bits 64 - sh .. of v (none for sh = 0)
+    __hip_atomic_fetch_or(w + i, (uint32_t)lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(w + i + 1, (uint32_t)(lo >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(w + i + 2, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    pos += n;
+  }
+  __device__ __forceinline__ void skip(uint32_t n) { pos += n; }
+};
+
+__device__ __forceinline__ uint32_t bfe8(uint32_t x, uint32_t o) { return (x >> o) & 255u; }
+
+template <class W>
+__device__ __forceinline__ void encode_plane64_dup(W& w, uint64_t P, uint32_t& bits, uint32_t& n, const uint32_t* dup)
+{
+  const bool full = n >= 64;
+  const uint64_t r = full ? 0ull : P >> (n & 63u);
+  const uint64_t V = full ? P : ((P & lowmask64(n)) | ((uint64_t)(r != 0) << n));
+  const uint32_t vn = full ? 64u : n + 1u;
+  w.put(V, vn);
+  bits += vn;
+  if (r != 0) {
+    const uint32_t rl = (uint32_t)r, rh = (uint32_t)(r >> 32);
+    const uint32_t hb = rh ? 63u - (uint32_t)__builtin_clz(rh) : 31u - (uint32_t)__builtin_clz(rl);
+    const uint32_t m = (uint32_t)__builtin_popcount(rl) + (uint32_t)__builtin_popcount(rh);
+    // E(r_lo): chunk c of r starts at 8c + popcount(r[0 .. 8c-1]) <= 48, so four 16-bit codes fit in 64 bits
+    uint64_t E0 = dup[rl & 255u];
+    uint32_t off = 8u + (uint32_t)__builtin_popcount(rl & 255u);
+#pragma unroll
+    for (uint32_t c = 1; c < 4; c++) {
+      if (!__any(hb >= 8 * c)) break;
+      const uint32_t v = bfe8(rl, 8 * c);
+      E0 |= (uint64_t)dup[v] << off;
+      off += 8u + (uint32_t)__builtin_popcount(v);
+    }
+    const uint32_t nout = n + hb + 1u;
+    const uint32_t keep = hb + m - (nout >= 64 ? 1u : 0u);  // bits of E(r) written
+    const uint32_t glen = keep + (nout < 64 ? 1u : 0u);     // and the closing '0'
+    uint64_t E1 = 0;
+    if (__any(hb >= 32)) {  // E(r_hi) after E(r_lo) (off = 32 + popcount(r_lo) there)
+      uint64_t Eh = dup[rh & 255u];
+      uint32_t oh = 8u + (uint32_t)__builtin_popcount(rh & 255u);
+#pragma unroll
+      for (uint32_t c = 1; c < 4; c++) {
+        if (!__any(hb >= 32 + 8 * c)) break;
+        const uint32_t v = bfe8(rh, 8 * c);
+        Eh |= (uint64_t)dup[v] << oh;
+        oh += 8u + (uint32_t)__builtin_popcount(v);
+      }
+      if (hb >= 32) {
+        E0 |= off < 64 ? Eh << off : 0ull;
+        E1 = (Eh >> 1) >> (63u - (off & 63u));  // off in 32 .. 64: bits of Eh past E0's 64
+        E1 = off >= 64 ? Eh : E1;
+      }
+    }
+    w.put(E0 & lowmask64(keep), glen < 64 ? glen : 64u);
+    if (glen > 64) w.put(E1 & lowmask64(keep - 64u), glen - 64u);
+    bits += glen;
+    n = nout;
+  }
+}
+
+template <int K, class W>
+__device__ __forceinline__ void encode_planes64_dup(W& w, const uint32_t* t, int kstart, int kmin, uint32_t budget,
+                                                    uint32_t& bits, uint32_t& n, const uint32_t* dup)
+{
+  if constexpr (K >= 0) {
+    if (K < kmin || bits >= budget) return;
+    if (K <= kstart) encode_plane64_dup(w, (uint64_t)t[K] | ((uint64_t)t[32 + K] << 32), bits, n, dup);
+    encode_planes64_dup<K - 1>(w, t, kstart, kmin, budget, bits, n, dup);
+  }
+}
+
+// encode_ints (encode.c:279-408) for 64 coefficients with the plane coder above: the planes above the highest
+// one-bit (n = 0, r = 0: one '0' each) are appended as one run of zeros. u is transposed in place.
+template <class W>
+__device__ __forceinline__ uint32_t encode_ints64_dup(W& w, uint32_t* u, uint32_t budget, uint32_t maxprec,
+                                                      const uint32_t* dup)
+{
+  const int kmin = maxprec < 32 ? 32 - (int)maxprec : 0;
+  uint32_t any = 0;
+#pragma unroll
+  for (int i = 0; i < 64; i++) any |= u[i];
+  // the planes are materialised stage by stage: left to itself the scheduler interleaves the two transposes and
+  // sinks their last stages into the plane code, keeping their inputs live across it (208 VGPRs instead of ~100)
+  asm volatile("" : "+v"(any));
+  pin32(u);
+  pin32(u + 32);
+  transpose32_pinned(u);
+  transpose32_pinned(u + 32);
+  const int top = any ? 31 - (int)__builtin_clz(any) : -1;  // highest plane with a one-bit
+  const int kstart = max(top, kmin - 1);
+  uint32_t bits = min((uint32_t)(31 - kstart), budget);
+  w.skip(bits);
+  uint32_t n = 0;
+  encode_planes64_dup<31>(w, u, kstart, kmin, budget, bits, n, dup);
+  return bits < budget ? bits : budget;
+}
+
 __device__ __forceinline__ bool exceeded_maxbits(uint32_t maxbits, uint32_t maxprec, uint32_t size)
 {
   return (maxprec + 1) * size - 1 > maxbits;  // common.c:232-236
 }
 
-// encode_fblock (encode.c:457-495) + encode_iblock (encode.c:412-455). Returns the block's bit count.
+// encode_fblock (encode.c:457-495) + encode_iblock (encode.c:412-455). Returns the block's bit count. With the
+// E-table `dup` (DupTab in LDS), 64-coefficient blocks take the plane coder encode_ints64_dup.
 template <int D, class W>
-__device__ __forceinline__ uint32_t encode_block(W& w, const float* f, const Params& p)
+__device__ __forceinline__ uint32_t encode_block(W& w, const float* f, const Params& p, const uint32_t* dup = nullptr)
 {
   constexpr int B = Dim<D>::B;
   float fa[B];
@@ -426,7 +590,9 @@ __device__ __forceinline__ uint32_t encode_block(W& w, const float* f, const Par
   const uint32_t maxb = p.maxbits - 9u;
   const uint32_t minb = p.minbits - (p.minbits < 9u ? p.minbits : 9u);
   const uint32_t budget = exceeded_maxbits(maxb, prec, B) ? maxb : 0xffffffffu;
-  uint32_t bits = encode_ints<B>(w, u, budget, prec);
+  uint32_t bits;
+  if constexpr (B == 64) bits = dup ? encode_ints64_dup(w, u, budget, prec, dup) : encode_ints<B>(w, u, budget, prec);
+  else bits = encode_ints<B>(w, u, budget, prec);
   if (bits < minb) {
     w.skip(minb - bits);
     bits = minb;

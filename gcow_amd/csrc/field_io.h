@@ -74,7 +74,7 @@ __device__ __forceinline__ void gather_block(const FieldDesc& F, uint32_t b, flo
         load_row4<DT>(F.data, base + (int64_t)y * F.s[1] + (int64_t)z * F.s[2], f + 16 * z + 4 * y);
   } else {
 #pragma unroll
-    for (int z = 0; z < (D > 2 ? 4 : 1); z++)
+    for (int z = 0; z < (D > 2 ? 4 : 1); z++) {
 #pragma unroll
       for (int y = 0; y < (D > 1 ? 4 : 1); y++)
 #pragma unroll
@@ -84,6 +84,11 @@ __device__ __forceinline__ void gather_block(const FieldDesc& F, uint32_t b, flo
           if (D > 2) off += (int64_t)pad_index(z, nvz) * F.s[2];
           f[16 * z + 4 * y + x] = load_elem<DT>(F.data, base + off);
         }
+      // one z-slice of loads in flight at a time: hoisting all 64 addresses (64-bit each) would cost 128 VGPRs
+      if constexpr (D > 2)
+#pragma unroll
+        for (int i = 0; i < 16; i++) asm volatile("" : "+v"(f[16 * z + i]));
+    }
   }
 }
 

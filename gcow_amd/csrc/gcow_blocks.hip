@@ -10,6 +10,11 @@
 
 namespace gcow {
 
+// Slack words after a 3-D fixed-rate block's budget in k_encode3d_fixed: a plane that starts inside the budget
+// appends at most 1 + 64 verbatim/flag bits and 129 group bits (encode_plane64_dup) -- 194 bits, 7 words from any
+// bit offset -- before the budget check stops the lane.
+constexpr uint32_t E3_SLACK = 8;
+
 // ------------------------------------------------------------------------------------------------ 3-D fixed rate
 // Fixed-rate 3-D blocks whose budget is a whole number of 32-bit words (maxbits = 32 WPB; rates 1, 2, 4, 8, 16, 32):
 // one block per lane, 256 consecutive blocks per workgroup. The lane codes its block (generic 64-coefficient coder,
@@ -18,21 +23,24 @@ namespace gcow {
 template <int DT, uint32_t WPB>
 __global__ __launch_bounds__(256) void k_encode3d_fixed(FieldDesc F, Params p, uint32_t* __restrict__ out32)
 {
-  extern __shared__ uint32_t lds_w[];  // 256 x (WPB + 1) words (odd stride: conflict-free per-lane words)
+  constexpr uint32_t STRIDE = WPB + E3_SLACK + 1;  // odd: lanes' words spread over the banks
+  extern __shared__ uint32_t lds_w[];               // 256 x STRIDE words, then the E table
+  uint32_t* dup = lds_w + 256 * STRIDE;
   const uint32_t tid = threadIdx.x;
   const uint32_t b0 = blockIdx.x * 256u;
   const uint32_t nvalid = min(256u, F.nblocks - b0);
-  uint32_t* mine = lds_w + tid * (WPB + 1);
+  dup[tid] = g_dup_tab.v[tid];
+  for (uint32_t j = tid; j < 64 * STRIDE; j += 256) ((uint4*)lds_w)[j] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
   if (tid < nvalid) {
     float f[64];
     gather_block<3, DT>(F, b0 + tid, f);
-    LaneWordWriter w{mine, 0ull, 0u, 0u, WPB * 32u};
-    encode_block<3>(w, f, p);
-    w.finish(mine + WPB);
+    OrWriter w{lds_w + tid * STRIDE, 0u};
+    encode_block<3>(w, f, p, dup);
   }
   __syncthreads();
   uint32_t* dst = out32 + (uint64_t)b0 * WPB;
-  for (uint32_t j = tid; j < nvalid * WPB; j += 256) dst[j] = lds_w[(j / WPB) * (WPB + 1) + (j % WPB)];
+  for (uint32_t j = tid; j < nvalid * WPB; j += 256) dst[j] = lds_w[(j / WPB) * STRIDE + (j % WPB)];
   if (blockIdx.x == gridDim.x - 1 && tid == 0 && (((uint64_t)F.nblocks * WPB) & 1))
     out32[(uint64_t)F.nblocks * WPB] = 0u;  // stream_flush: zero-pad to a 64-bit boundary
 }
@@ -184,7 +192,7 @@ hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in
 template <int DT, uint32_t WPB>
 static hipError_t launch_enc3d_t(const FieldDesc& F, const Params& p, uint32_t* out32, hipStream_t st)
 {
-  const size_t lds = 256 * (WPB + 1) * 4;
+  const size_t lds = (256 * (WPB + E3_SLACK + 1) + 256) * 4;
   auto kern = k_encode3d_fixed<DT, WPB>;
   if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   kern<<<(F.nblocks + 255) / 256, 256, lds, st>>>(F, p, out32);
