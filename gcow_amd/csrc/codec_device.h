@@ -620,7 +620,8 @@ __device__ __forceinline__ uint32_t encode_ints_length(const uint32_t* u, uint32
   int Rn = Llast;  // R_{j+1}
 #pragma unroll
   for (int j = B - 2; j >= 0; j--) {
-    const int Lj = u[j] ? 31 - (int)__builtin_clz(u[j]) : -1;
+    int Lj = u[j] ? 31 - (int)__builtin_clz(u[j]) : -1;
+    asm volatile("" : "+v"(Lj));  // in order: hoisting all 64 leading-plane counts costs 64 VGPRs
     const int Rj = max(Lj, Rn);
     const bool on = Rj >= kmin;
     len += max(Rj, kmin);
@@ -657,6 +658,65 @@ __device__ __forceinline__ uint32_t count_block(const float* f, const Params& p)
   uint32_t bits = encode_ints_length<B>(u, prec);
   bits = bits < budget ? bits : budget;
   return 9 + (bits < minb ? minb : bits);
+}
+
+// encode_fblock split in three for the two-pass tile encoder, which needs a block's length before it can place the
+// block: prepare (header fields; cast, transform and reorder into u), length (count_block's value), code (the
+// bits, encode_block's value). The coefficients are derived once instead of once per pass.
+struct BlockHead {
+  uint32_t be;      // biased exponent, 0 = empty block (a single '0' bit)
+  uint32_t prec;    // get_precision
+  uint32_t budget;  // encode_ints' bit budget (maxbits - 9, or unlimited)
+  uint32_t minb;    // pad target after the header
+};
+
+template <int D>
+__device__ __forceinline__ BlockHead prepare_block(const float* f, const Params& p, uint32_t* u)
+{
+  constexpr int B = Dim<D>::B;
+  float fa[B];
+#pragma unroll
+  for (int i = 0; i < B; i++) fa[i] = f[i];
+  const int emax = block_emax<B>(fa);
+  BlockHead h;
+  h.prec = precision(emax, p.maxprec, p.minexp, D);
+  h.be = h.prec ? (uint32_t)(emax + 127) : 0u;
+  int32_t q[B];
+  const float s = cast_scale(emax);
+#pragma unroll
+  for (int i = 0; i < B; i++) q[i] = cast1(fa[i], s);
+  fwd_xform<D>(q);
+  fwd_reorder<D>(u, q);
+  const uint32_t maxb = p.maxbits - 9u;
+  h.minb = p.minbits - (p.minbits < 9u ? p.minbits : 9u);
+  h.budget = exceeded_maxbits(maxb, h.prec, B) ? maxb : 0xffffffffu;
+  return h;
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t block_length(const BlockHead& h, const uint32_t* u, const Params& p)
+{
+  if (!h.be) return p.minbits > 1u ? p.minbits : 1u;
+  uint32_t bits = encode_ints_length<B>(u, h.prec);
+  bits = bits < h.budget ? bits : h.budget;
+  return 9 + (bits < h.minb ? h.minb : bits);
+}
+
+template <int D, class W>
+__device__ __forceinline__ uint32_t code_block(W& w, const BlockHead& h, uint32_t* u, const Params& p,
+                                               const uint32_t* dup = nullptr)
+{
+  constexpr int B = Dim<D>::B;
+  if (!h.be) {
+    const uint32_t n = p.minbits > 1u ? p.minbits : 1u;  // a '0', padded with zeros to minbits
+    w.skip(n);
+    return n;
+  }
+  w.put(2ull * h.be + 1ull, 9);
+  uint32_t bits;
+  if constexpr (B == 64) bits = dup ? encode_ints64_dup(w, u, h.budget, h.prec, dup) : encode_ints<B>(w, u, h.budget, h.prec);
+  else bits = encode_ints<B>(w, u, h.budget, h.prec);
+  return 9 + (bits < h.minb ? h.minb : bits);
 }
 
 // ------------------------------------------------------------------------------------------------ reader / decoder
@@ -750,6 +810,54 @@ __device__ __forceinline__ uint32_t decode_ints(Rd& r, uint32_t maxbits, uint32_
   return maxbits - bits;
 }
 
+// decode_ints for 64 coefficients: plane k goes to t[k] (coefficients 0..31) / t[32 + k] (32..63) with a
+// compile-time index, and one pair of 32 x 32 bit transposes at the end turns the planes into coefficients -- instead
+// of depositing every plane's 64 bits into 64 coefficient words (three operations per coefficient per plane).
+template <int K, class Rd>
+__device__ __forceinline__ void decode_planes64(Rd& r, int kmin, uint32_t& bits, uint32_t& n, uint32_t* t)
+{
+  if constexpr (K >= 0) {
+    uint64_t x = 0;
+    if (bits && K >= kmin) {
+      const uint32_t m = n < bits ? n : bits;
+      bits -= m;
+      x = r.get(m);
+      while (n < 64u && bits) {
+        bits--;
+        if (!r.bit()) break;  // negative group test
+        const uint32_t lim = min(63u - n, bits);
+        const uint64_t w = r.peek64();
+        const uint32_t z = w ? (uint32_t)__builtin_ctzll(w) : 64u;
+        if (z < lim) {
+          r.pos += z + 1;
+          bits -= z + 1;
+          n += z;
+        } else {
+          r.pos += lim;
+          bits -= lim;
+          n += lim;
+        }
+        x += 1ull << n;
+        n++;
+      }
+    }
+    t[K] = (uint32_t)x;
+    t[32 + K] = (uint32_t)(x >> 32);
+    decode_planes64<K - 1>(r, kmin, bits, n, t);
+  }
+}
+
+template <class Rd>
+__device__ __forceinline__ uint32_t decode_ints64(Rd& r, uint32_t maxbits, uint32_t maxprec, uint32_t* u)
+{
+  const int kmin = maxprec < 32 ? 32 - (int)maxprec : 0;
+  uint32_t bits = maxbits, n = 0;
+  decode_planes64<31>(r, kmin, bits, n, u);
+  transpose32(u);
+  transpose32(u + 32);
+  return maxbits - bits;
+}
+
 // dequantize (decode.c:12-25): ldexpf(1, emax - 30) exactly, including subnormal and zero scales.
 __device__ __forceinline__ float dequant_scale(int emax)
 {
@@ -773,7 +881,9 @@ __device__ __forceinline__ void decode_block(Rd& r, const Params& p, float* f)
     const uint32_t maxb = p.maxbits - bits;
     uint32_t u[B];
     const uint32_t budget = exceeded_maxbits(maxb, prec, B) ? maxb : 0xffffffffu;
-    uint32_t got = decode_ints<B>(r, budget, prec, u);
+    uint32_t got;
+    if constexpr (B == 64) got = decode_ints64(r, budget, prec, u);
+    else got = decode_ints<B>(r, budget, prec, u);
     if (got < minb) r.pos += minb - got;
     int32_t q[B];
     inv_reorder<D>(q, u);

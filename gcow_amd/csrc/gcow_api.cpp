@@ -124,6 +124,8 @@ gcow::TilePlan make_plan(const gcow::FieldDesc& F, const gcow_params& p)
   pl.threads = F.dims == 3 ? 64 : (U <= 2048 ? 256 : 64);
   if (pl.fixed) {
     pl.range = pl.threads;
+  } else if (F.dims == 3) {
+    pl.range = 64;  // one 64-block tile per workgroup (gcow_blocks.hip k_count3d / k_encode3d_var)
   } else {
     const uint64_t target = 2048;
     uint64_t r = (F.nblocks + target - 1) / target;

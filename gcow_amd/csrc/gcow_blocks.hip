@@ -20,8 +20,11 @@ constexpr uint32_t E3_SLACK = 8;
 // one block per lane, 256 consecutive blocks per workgroup. The lane codes its block (generic 64-coefficient coder,
 // encode.c:457-495 with libzfp's 3-D transform and perm_3) into its own LDS words through LaneWordWriter -- whole
 // words, no atomics -- and the workgroup then stores its 256 WPB contiguous stream words coalesced.
+// Held to 128 VGPRs (4 waves per SIMD; 22 VGPRs spill): C3 rate 8 0.225 -> 0.211 ms. The same bound on the tile
+// kernels spills in their hot loop (C3 accuracy 1e-3: 0.591 -> 0.829 ms), so they are left alone
+// (profiles/r02_c3_occupancy_ab.log).
 template <int DT, uint32_t WPB>
-__global__ __launch_bounds__(256) void k_encode3d_fixed(FieldDesc F, Params p, uint32_t* __restrict__ out32)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_encode3d_fixed(FieldDesc F, Params p, uint32_t* __restrict__ out32)
 {
   constexpr uint32_t STRIDE = WPB + E3_SLACK + 1;  // odd: lanes' words spread over the banks
   extern __shared__ uint32_t lds_w[];               // 256 x STRIDE words, then the E table
@@ -43,6 +46,97 @@ __global__ __launch_bounds__(256) void k_encode3d_fixed(FieldDesc F, Params p, u
   for (uint32_t j = tid; j < nvalid * WPB; j += 256) dst[j] = lds_w[(j / WPB) * STRIDE + (j % WPB)];
   if (blockIdx.x == gridDim.x - 1 && tid == 0 && (((uint64_t)F.nblocks * WPB) & 1))
     out32[(uint64_t)F.nblocks * WPB] = 0u;  // stream_flush: zero-pad to a 64-bit boundary
+}
+
+// ------------------------------------------------------------------------------------------------ 3-D variable rate
+// Two passes over tiles of 64 blocks, one tile (one wave) per workgroup and no loop inside: a loop over tiles keeps
+// loop-carried state next to the 64 coefficients (152-179 VGPRs against 113 for one block), one tile per workgroup
+// does not, and 32 Ki workgroups for a 512^3 field still fill the chip.
+//   k_count3d   block lengths (closed form, codec_device.h block_length) summed per tile -> sums[tile]
+//   k_scan_ranges (gcow_kernels.hip) turns the sums into tile bit offsets and zeroes the words two tiles share
+//   k_encode3d_var  re-derives the coefficients and the lengths, a wave prefix sum places each block in an LDS window
+//                   of the tile, the plane coder ORs the block's bits in, and the window is stored coalesced (the two
+//                   edge words shared with the neighbouring tiles by atomicOr).
+// MASK: some block may hit the bit budget (exceeded_maxbits for maxprec), so writes are clipped at the block's end
+// (LdsWriter); otherwise every block writes exactly its length and the unclipped OrWriter is used.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane)
+{
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    x += lane >= (uint32_t)o ? y : 0u;
+  }
+  return x;
+}
+
+template <int DT>
+__global__ __launch_bounds__(64) void k_count3d(FieldDesc F, Params p, uint64_t* __restrict__ sums)
+{
+  const uint32_t b = blockIdx.x * 64u + threadIdx.x;
+  uint32_t len = 0;
+  if (b < F.nblocks) {
+    float f[64];
+    gather_block<3, DT>(F, b, f);
+    uint32_t u[64];
+    const BlockHead h = prepare_block<3>(f, p, u);
+    len = block_length<64>(h, u, p);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) len += __shfl_xor(len, o, 64);
+  if (threadIdx.x == 0) sums[blockIdx.x] = len;
+}
+
+template <int DT, bool MASK>
+__global__ __launch_bounds__(64) void k_encode3d_var(FieldDesc F, Params p, const uint64_t* __restrict__ rbase,
+                                                     uint32_t* __restrict__ out32, uint64_t* __restrict__ index,
+                                                     uint32_t index_shift)
+{
+  extern __shared__ uint32_t win[];  // the tile's bits, plus 2 words for the writers' third word
+  __shared__ uint32_t dup[256];
+  const uint32_t lane = threadIdx.x;
+#pragma unroll
+  for (uint32_t t = 0; t < 4; t++) dup[lane + 64 * t] = g_dup_tab.v[lane + 64 * t];
+  const uint32_t b = blockIdx.x * 64u + lane;
+  const bool valid = b < F.nblocks;
+  uint32_t u[64];
+  BlockHead h{};
+  uint32_t len = 0;
+  if (valid) {
+    float f[64];
+    gather_block<3, DT>(F, b, f);
+    h = prepare_block<3>(f, p, u);
+    len = block_length<64>(h, u, p);
+  }
+  const uint32_t incl = wave_incl_scan(len, lane);
+  const uint32_t excl = incl - len, total = __shfl(incl, 63, 64);
+  const uint64_t base = rbase[blockIdx.x];
+  const uint32_t lb = (uint32_t)(base & 31);
+  const uint32_t W = (lb + total + 31) >> 5;
+  for (uint32_t j = lane; j < W + 2; j += 64) win[j] = 0u;
+  __syncthreads();
+  if (valid) {
+    if constexpr (MASK) {
+      LdsWriter w{win, lb + excl, lb + excl + len};
+      code_block<3>(w, h, u, p, dup);
+    } else {
+      OrWriter w{win, lb + excl};
+      code_block<3>(w, h, u, p, dup);
+    }
+    if (index && (b & ((1u << index_shift) - 1)) == 0) index[b >> index_shift] = base + excl;
+  }
+  __syncthreads();
+  const uint64_t gw0 = base >> 5;
+  const bool last = blockIdx.x == gridDim.x - 1;
+  const bool tail_shared = ((lb + total) & 31) != 0 && !last;
+  for (uint32_t j = lane; j < W; j += 64) {
+    const uint32_t v = win[j];
+    if ((j == 0 && lb != 0) || (j == W - 1 && tail_shared)) atomicOr(out32 + gw0 + j, v);
+    else out32[gw0 + j] = v;
+  }
+  if (last && lane == 0) {
+    const uint64_t endw = (base + total + 31) >> 5;  // stream_flush: zero-pad to a 64-bit boundary
+    if (endw & 1) out32[endw] = 0u;
+  }
 }
 
 // The matching decoder: the workgroup stages its 256 blocks' stream words in LDS (coalesced), each lane decodes its
@@ -144,6 +238,18 @@ static hipError_t launch_tiles23_t(const FieldDesc& F, const Params& p, const Ti
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     kern<<<plan.nranges, T, lds, st>>>(F, p, plan.range, nullptr, out32, index, index_shift);
     return hipGetLastError();
+  }
+  if constexpr (D == 3) {
+    if (plan.range == 64) {  // one tile per workgroup (make_plan): k_count3d / k_encode3d_var
+      k_count3d<DT><<<plan.nranges, 64, 0, st>>>(F, p, ws_sums);
+      hipError_t e = launch_scan_ranges(ws_sums, plan.nranges, ws_base, d_total, out32, d_base, st);
+      if (e != hipSuccess) return e;
+      const bool mask = (p.maxprec + 1) * 64u - 1u > p.maxbits - 9u;  // exceeded_maxbits at maxprec: a budget can clip
+      auto kern = mask ? k_encode3d_var<DT, true> : k_encode3d_var<DT, false>;
+      if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      kern<<<plan.nranges, 64, lds, st>>>(F, p, ws_base, out32, index, index_shift);
+      return hipGetLastError();
+    }
   }
   k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   hipError_t e = launch_scan_ranges(ws_sums, plan.nranges, ws_base, d_total, out32, d_base, st);

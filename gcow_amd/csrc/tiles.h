@@ -73,7 +73,12 @@ __global__ __launch_bounds__(T) void k_encode_tiles(FieldDesc F, Params p, uint3
   constexpr int B = Dim<D>::B;
   extern __shared__ uint32_t lds[];
   __shared__ uint32_t scan_sh[T / 64 > 0 ? T / 64 : 1];
+  __shared__ uint32_t dup[B == 64 ? 256 : 1];  // E table of the 64-coefficient plane coder
   const uint32_t tid = threadIdx.x;
+  if constexpr (B == 64) {
+    for (uint32_t t = tid; t < 256; t += T) dup[t] = g_dup_tab.v[t];
+    __syncthreads();
+  }
   const uint64_t b0 = (uint64_t)blockIdx.x * range;
   const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
   const bool final_range = b1 == F.nblocks;
@@ -84,15 +89,14 @@ __global__ __launch_bounds__(T) void k_encode_tiles(FieldDesc F, Params p, uint3
   for (uint64_t t0 = b0; t0 < b1; t0 += T) {
     const uint64_t b = t0 + tid;
     const bool valid = b < b1;
-    float f[B];
+    uint32_t u[B];
+    BlockHead h{};
     uint32_t len = 0;
     if (valid) {
+      float f[B];
       gather_block<D, DT>(F, (uint32_t)b, f);
-      if (FIXED) {
-        len = p.maxbits;
-      } else {
-        len = count_block<D>(f, p);
-      }
+      h = prepare_block<D>(f, p, u);
+      len = FIXED ? p.maxbits : block_length<B>(h, u, p);
     }
     uint32_t tile_total;
     const uint32_t excl = block_exclusive_scan<T>(len, &tile_total, scan_sh);
@@ -103,7 +107,7 @@ __global__ __launch_bounds__(T) void k_encode_tiles(FieldDesc F, Params p, uint3
     __syncthreads();
     if (valid) {
       LdsWriter w{lds, lbase + excl, lbase + excl + len};
-      encode_block<D>(w, f, p);
+      code_block<D>(w, h, u, p, B == 64 ? dup : nullptr);
       if (index && ((b & ((1ull << index_shift) - 1)) == 0)) index[b >> index_shift] = base + excl;
     }
     __syncthreads();

@@ -22,6 +22,9 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+if "--lib" in sys.argv:  # A/B: time another build of libgcow.so (e.g. ab/variant.so)
+    from gcow_amd import _ffi  # noqa: E402
+    _ffi.LIB_PATH = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
 from gcow_amd import codec  # noqa: E402
 
 
@@ -155,6 +158,9 @@ def c5():
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("cases", nargs="*", default=["c2_decode", "c3", "var_f32", "c5"])
+    ap.add_argument("--lib", default=None, help="libgcow.so to load instead of the in-tree build")
     a = ap.parse_args()
+    if a.lib:
+        print("lib", a.lib, flush=True)
     for c in a.cases:
         globals()[c]()
