@@ -10,6 +10,9 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+if "--lib" in sys.argv:  # A/B: profile another build of libgcow.so
+    from gcow_amd import _ffi  # noqa: E402
+    _ffi.LIB_PATH = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
 from gcow_amd import codec  # noqa: E402
 
 
@@ -58,6 +61,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("cases", nargs="*", default=["c3", "c5"])
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--lib", default=None, help="libgcow.so to load instead of the in-tree build")
     a = ap.parse_args()
     for c in a.cases:
         globals()[c](a.reps)
