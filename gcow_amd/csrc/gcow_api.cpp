@@ -772,7 +772,9 @@ size_t gcow_encode_workspace_bytes(const zfp_input* field, const gcow_params* p)
   if (make_field(field, F, false) || !p || p->minbits == p->maxbits) return 0;
   if (F.dims == 4) return (size_t)F.nblocks * 4 + (2 * (size_t)F.nblocks + 1) * 8 + 16;  // lens, sums, base
   const gcow::TilePlan pl = make_plan(F, *p);
-  return (2 * (size_t)pl.nranges + 1) * 8;
+  // sums, base; 3-D variable rate also keeps every block's length (uint16) from the count pass for the encode pass
+  const size_t lens = F.dims == 3 ? ((size_t)F.nblocks * 2 + 7) / 8 * 8 : 0;
+  return (2 * (size_t)pl.nranges + 1) * 8 + lens;
 }
 
 size_t gcow_index_entries(const zfp_input* field, uint32_t index_stride)

@@ -54,7 +54,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // does not, and 32 Ki workgroups for a 512^3 field still fill the chip.
 //   k_count3d   block lengths (closed form, codec_device.h block_length) summed per tile -> sums[tile]
 //   k_scan_ranges (gcow_kernels.hip) turns the sums into tile bit offsets and zeroes the words two tiles share
-//   k_encode3d_var  re-derives the coefficients and the lengths, a wave prefix sum places each block in an LDS window
+//   k_encode3d_var  re-derives the coefficients (the lengths come from k_count3d through the workspace), a wave
+//                   prefix sum places each block in an LDS window
 //                   of the tile, the plane coder ORs the block's bits in, and the window is stored coalesced (the two
 //                   edge words shared with the neighbouring tiles by atomicOr).
 // MASK: some block may hit the bit budget (exceeded_maxbits for maxprec), so writes are clipped at the block's end
@@ -70,7 +71,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane)
 }
 
 template <int DT>
-__global__ __launch_bounds__(64) void k_count3d(FieldDesc F, Params p, uint64_t* __restrict__ sums)
+__global__ __launch_bounds__(64) void k_count3d(FieldDesc F, Params p, uint64_t* __restrict__ sums,
+                                                uint16_t* __restrict__ lens)
 {
   const uint32_t b = blockIdx.x * 64u + threadIdx.x;
   uint32_t len = 0;
@@ -80,6 +82,7 @@ __global__ __launch_bounds__(64) void k_count3d(FieldDesc F, Params p, uint64_t*
     uint32_t u[64];
     const BlockHead h = prepare_block<3>(f, p, u);
     len = block_length<64>(h, u, p);
+    lens[b] = (uint16_t)len;  // <= 9 + 64 * 33 bits
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) len += __shfl_xor(len, o, 64);
@@ -88,8 +91,8 @@ __global__ __launch_bounds__(64) void k_count3d(FieldDesc F, Params p, uint64_t*
 
 template <int DT, bool MASK>
 __global__ __launch_bounds__(64) void k_encode3d_var(FieldDesc F, Params p, const uint64_t* __restrict__ rbase,
-                                                     uint32_t* __restrict__ out32, uint64_t* __restrict__ index,
-                                                     uint32_t index_shift)
+                                                     const uint16_t* __restrict__ lens, uint32_t* __restrict__ out32,
+                                                     uint64_t* __restrict__ index, uint32_t index_shift)
 {
   extern __shared__ uint32_t win[];  // the tile's bits, plus 2 words for the writers' third word
   __shared__ uint32_t dup[256];
@@ -102,10 +105,10 @@ __global__ __launch_bounds__(64) void k_encode3d_var(FieldDesc F, Params p, cons
   BlockHead h{};
   uint32_t len = 0;
   if (valid) {
+    len = lens[b];
     float f[64];
     gather_block<3, DT>(F, b, f);
     h = prepare_block<3>(f, p, u);
-    len = block_length<64>(h, u, p);
   }
   const uint32_t incl = wave_incl_scan(len, lane);
   const uint32_t excl = incl - len, total = __shfl(incl, 63, 64);
@@ -241,13 +244,14 @@ static hipError_t launch_tiles23_t(const FieldDesc& F, const Params& p, const Ti
   }
   if constexpr (D == 3) {
     if (plan.range == 64) {  // one tile per workgroup (make_plan): k_count3d / k_encode3d_var
-      k_count3d<DT><<<plan.nranges, 64, 0, st>>>(F, p, ws_sums);
+      uint16_t* lens = (uint16_t*)(ws_base + plan.nranges + 1);  // workspace: sums, base, lens
+      k_count3d<DT><<<plan.nranges, 64, 0, st>>>(F, p, ws_sums, lens);
       hipError_t e = launch_scan_ranges(ws_sums, plan.nranges, ws_base, d_total, out32, d_base, st);
       if (e != hipSuccess) return e;
       const bool mask = (p.maxprec + 1) * 64u - 1u > p.maxbits - 9u;  // exceeded_maxbits at maxprec: a budget can clip
       auto kern = mask ? k_encode3d_var<DT, true> : k_encode3d_var<DT, false>;
       if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      kern<<<plan.nranges, 64, lds, st>>>(F, p, ws_base, out32, index, index_shift);
+      kern<<<plan.nranges, 64, lds, st>>>(F, p, ws_base, lens, out32, index, index_shift);
       return hipGetLastError();
     }
   }
