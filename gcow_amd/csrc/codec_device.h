@@ -464,6 +464,30 @@ struct OrWriter {
   __device__ __forceinline__ void skip(uint32_t n) { pos += n; }
 };
 
+// The same appends straight into a global stream (atomicOr), clipped at the block's end: the fallback for a tile
+// whose bits do not fit its LDS window. Only nonzero words are touched (nothing past the clipped code).
+struct GlobalOrWriter {
+  uint32_t* w;
+  uint64_t pos, limit;
+  __device__ __forceinline__ void put(uint64_t v, uint32_t n)
+  {
+    if (pos >= limit || n == 0) {
+      pos += n;
+      return;
+    }
+    if (n > limit - pos) v &= lowmask64((uint32_t)(limit - pos));
+    const uint64_t i = pos >> 5;
+    const uint32_t sh = (uint32_t)(pos & 31u);
+    const uint64_t lo = v << sh;
+    const uint32_t hi = (uint32_t)((v >> 1) >> (63u - sh));
+    if ((uint32_t)lo) atomicOr(w + i, (uint32_t)lo);
+    if ((uint32_t)(lo >> 32)) atomicOr(w + i + 1, (uint32_t)(lo >> 32));
+    if (hi) atomicOr(w + i + 2, hi);
+    pos += n;
+  }
+  __device__ __forceinline__ void skip(uint32_t n) { pos += n; }
+};
+
 __device__ __forceinline__ uint32_t bfe8(uint32_t x, uint32_t o) { return (x >> o) & 255u; }
 
 template <class W>

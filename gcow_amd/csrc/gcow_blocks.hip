@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "codec_device.h"
 #include "kernels.h"
 #include "tiles.h"
@@ -89,10 +91,15 @@ __global__ __launch_bounds__(64) void k_count3d(FieldDesc F, Params p, uint64_t*
   if (threadIdx.x == 0) sums[blockIdx.x] = len;
 }
 
+// The LDS window holds a tile of up to E3V_WIN_WORDS - 2 words (64 blocks of 24 bits per value on average): sized
+// for the worst case (64 x 2120 bits, 17 KB) it would cap the kernel at 9 workgroups per CU, i.e. 2.25 waves per
+// SIMD. A tile that does not fit zeroes its interior stream words and codes straight into global memory.
+constexpr uint32_t E3V_WIN_WORDS = 64 * 1536 / 32 + 2;
+
 template <int DT, bool MASK>
 __global__ __launch_bounds__(64) void k_encode3d_var(FieldDesc F, Params p, const uint64_t* __restrict__ rbase,
                                                      const uint16_t* __restrict__ lens, uint32_t* __restrict__ out32,
-                                                     uint64_t* __restrict__ index, uint32_t index_shift)
+                                                     uint64_t* __restrict__ index, uint32_t index_shift, uint32_t win_words)
 {
   extern __shared__ uint32_t win[];  // the tile's bits, plus 2 words for the writers' third word
   __shared__ uint32_t dup[256];
@@ -101,23 +108,46 @@ __global__ __launch_bounds__(64) void k_encode3d_var(FieldDesc F, Params p, cons
   for (uint32_t t = 0; t < 4; t++) dup[lane + 64 * t] = g_dup_tab.v[lane + 64 * t];
   const uint32_t b = blockIdx.x * 64u + lane;
   const bool valid = b < F.nblocks;
-  uint32_t u[64];
-  BlockHead h{};
-  uint32_t len = 0;
-  if (valid) {
-    len = lens[b];
-    float f[64];
-    gather_block<3, DT>(F, b, f);
-    h = prepare_block<3>(f, p, u);
-  }
+  // placement first (lengths from the count pass), so the 64 coefficients are live only from gather to code
+  const uint32_t len = valid ? lens[b] : 0u;
   const uint32_t incl = wave_incl_scan(len, lane);
   const uint32_t excl = incl - len, total = __shfl(incl, 63, 64);
   const uint64_t base = rbase[blockIdx.x];
   const uint32_t lb = (uint32_t)(base & 31);
   const uint32_t W = (lb + total + 31) >> 5;
+  const uint64_t gw0 = base >> 5;
+  const bool last = blockIdx.x == gridDim.x - 1;
+  const bool tail_shared = ((lb + total) & 31) != 0 && !last;
+  if (W + 2 > win_words) {  // oversized tile (wave-uniform): code into the zeroed stream words directly
+    for (uint32_t j = lane; j < W; j += 64)
+      if (!((j == 0 && lb != 0) || (j == W - 1 && tail_shared))) out32[gw0 + j] = 0u;  // edges zeroed by the scan
+    __threadfence();
+    __syncthreads();
+    if (valid) {
+      uint32_t u[64];
+      float f[64];
+      gather_block<3, DT>(F, b, f);
+      const BlockHead h = prepare_block<3>(f, p, u);
+      GlobalOrWriter w{out32, base + excl, base + excl + len};
+      code_block<3>(w, h, u, p, dup);
+      if (index && (b & ((1u << index_shift) - 1)) == 0) index[b >> index_shift] = base + excl;
+    }
+    if (last && lane == 0) {
+      const uint64_t endw = (base + total + 31) >> 5;
+      if (endw & 1) out32[endw] = 0u;
+    }
+    return;
+  }
   for (uint32_t j = lane; j < W + 2; j += 64) win[j] = 0u;
   __syncthreads();
   if (valid) {
+    uint32_t u[64];
+    BlockHead h;
+    {
+      float f[64];
+      gather_block<3, DT>(F, b, f);
+      h = prepare_block<3>(f, p, u);
+    }
     if constexpr (MASK) {
       LdsWriter w{win, lb + excl, lb + excl + len};
       code_block<3>(w, h, u, p, dup);
@@ -128,9 +158,6 @@ __global__ __launch_bounds__(64) void k_encode3d_var(FieldDesc F, Params p, cons
     if (index && (b & ((1u << index_shift) - 1)) == 0) index[b >> index_shift] = base + excl;
   }
   __syncthreads();
-  const uint64_t gw0 = base >> 5;
-  const bool last = blockIdx.x == gridDim.x - 1;
-  const bool tail_shared = ((lb + total) & 31) != 0 && !last;
   for (uint32_t j = lane; j < W; j += 64) {
     const uint32_t v = win[j];
     if ((j == 0 && lb != 0) || (j == W - 1 && tail_shared)) atomicOr(out32 + gw0 + j, v);
@@ -250,8 +277,8 @@ static hipError_t launch_tiles23_t(const FieldDesc& F, const Params& p, const Ti
       if (e != hipSuccess) return e;
       const bool mask = (p.maxprec + 1) * 64u - 1u > p.maxbits - 9u;  // exceeded_maxbits at maxprec: a budget can clip
       auto kern = mask ? k_encode3d_var<DT, true> : k_encode3d_var<DT, false>;
-      if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      kern<<<plan.nranges, 64, lds, st>>>(F, p, ws_base, lens, out32, index, index_shift);
+      const uint32_t win = std::min<uint32_t>(plan.lds_words, E3V_WIN_WORDS);
+      kern<<<plan.nranges, 64, (size_t)win * 4, st>>>(F, p, ws_base, lens, out32, index, index_shift, win);
       return hipGetLastError();
     }
   }

@@ -117,7 +117,7 @@ def test_1d_other_rates(gc, orc, r):
 
 
 @pytest.mark.parametrize("shape", [(1000,), (4096 * 3 + 1,), (37, 53), (64, 64), (9, 10, 7), (16, 20, 24)])
-@pytest.mark.parametrize("mode", ["acc3", "acc6", "prec12", "rate8", "expert"])
+@pytest.mark.parametrize("mode", ["acc3", "acc6", "prec12", "prec32", "rate8", "expert"])
 def test_random_all_dims(gc, orc, shape, mode):
     rng = np.random.default_rng(zlib.crc32(repr((shape, mode)).encode()))
     a = (rng.standard_normal(shape) * 1e-2).astype(np.float32)
@@ -125,8 +125,21 @@ def test_random_all_dims(gc, orc, shape, mode):
     flat[:: 97] = 0
     flat[5:9] = [1e-36, -2e-38, 7e-39, 0]  # tiny and subnormal members
     op = {"acc3": orc.accuracy(1e-3), "acc6": orc.accuracy(1e-6), "prec12": orc.precision(12),
-          "rate8": orc.rate(8, len(shape)), "expert": orc.expert(20, 160, 20, -30)}[mode]
+          "prec32": orc.precision(32), "rate8": orc.rate(8, len(shape)), "expert": orc.expert(20, 160, 20, -30)}[mode]
     _check_vs_oracle(gc, orc, a, op, index_stride=0 if op.minbits == op.maxbits else 2)
+
+
+@pytest.mark.parametrize("mode", ["prec32", "acc1e-30"])
+def test_3d_var_oversized_tiles(gc, orc, mode):
+    """3-D variable rate where some 64-block tiles exceed the LDS window (k_encode3d_var codes those straight into
+    global memory) next to tiles that fit: zero slabs between near-lossless noise, so fitting and oversized tiles
+    share edge words both ways."""
+    rng = np.random.default_rng(31 if mode == "prec32" else 32)
+    a = (rng.standard_normal((24, 40, 64)) * 1e-2).astype(np.float32)
+    a[4:12] = 0
+    a[16:20, :, :32] = 0
+    op = orc.precision(32) if mode == "prec32" else orc.accuracy(1e-30)
+    _check_vs_oracle(gc, orc, a, op, index_stride=1)
 
 
 def test_subnormal_cast_members(gc, orc):
