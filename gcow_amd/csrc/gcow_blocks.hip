@@ -255,7 +255,7 @@ __global__ __launch_bounds__(64) void k_decode_staged(FieldDesc F, Params p, con
 }
 
 // ------------------------------------------------------------------------------------------------ launchers
-static inline hipStream_t S(void* s) { return (hipStream_t)s; }
+static inline hipStream_t hip_stream(void* s) { return (hipStream_t)s; }
 
 template <int D, int DT, uint32_t T>
 static hipError_t launch_tiles23_t(const FieldDesc& F, const Params& p, const TilePlan& plan, uint32_t* out32,
@@ -295,7 +295,7 @@ hipError_t launch_encode_tiles23(const FieldDesc& F, const Params& p, const Tile
                                  uint64_t* ws_sums, uint64_t* ws_base, uint64_t* d_total, uint64_t* index,
                                  uint32_t index_shift, const uint64_t* d_base, void* stream)
 {
-  hipStream_t st = S(stream);
+  hipStream_t st = hip_stream(stream);
   const bool bf = F.dtype == DT_BF16;
 #define GCOW_TILES(D, T)                                                                                          \
   return bf ? launch_tiles23_t<D, DT_BF16, T>(F, p, plan, out32, ws_sums, ws_base, d_total, index, index_shift, d_base, st) \
@@ -313,16 +313,16 @@ hipError_t launch_decode(const FieldDesc& F, const Params& p, const uint64_t* in
 {
   if (chunk == 1 && in_words && (fixed || index) && F.dims >= 2) {
     const uint32_t g = (uint32_t)((F.nblocks + 63) / 64);
-    if (F.dims == 2) k_decode_staged<2><<<g, 64, 0, S(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
-    else k_decode_staged<3><<<g, 64, 0, S(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
+    if (F.dims == 2) k_decode_staged<2><<<g, 64, 0, hip_stream(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
+    else k_decode_staged<3><<<g, 64, 0, hip_stream(stream)>>>(F, p, in, in_words, index, fixed, base_bits, end_out);
     return hipGetLastError();
   }
   const uint32_t T = 64;
   const uint64_t grid = (nchunks + T - 1) / T;
   if (!grid) return hipSuccess;
-  if (F.dims == 1) k_decode<1><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
-  else if (F.dims == 2) k_decode<2><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
-  else k_decode<3><<<grid, T, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
+  if (F.dims == 1) k_decode<1><<<grid, T, 0, hip_stream(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
+  else if (F.dims == 2) k_decode<2><<<grid, T, 0, hip_stream(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
+  else k_decode<3><<<grid, T, 0, hip_stream(stream)>>>(F, p, in, index, chunk, nchunks, fixed, base_bits, end_out);
   return hipGetLastError();
 }
 
@@ -354,7 +354,7 @@ bool fixed3d_ok(uint32_t maxbits)
 
 hipError_t launch_encode3d_fixed(const FieldDesc& F, const Params& p, uint32_t* out32, void* stream)
 {
-  hipStream_t st = S(stream);
+  hipStream_t st = hip_stream(stream);
   const bool bf = F.dtype == DT_BF16;
 #define GCOW_E3(W) return bf ? launch_enc3d_t<DT_BF16, W>(F, p, out32, st) : launch_enc3d_t<DT_F32, W>(F, p, out32, st)
   switch (p.maxbits / 32) {
@@ -371,7 +371,7 @@ hipError_t launch_encode3d_fixed(const FieldDesc& F, const Params& p, uint32_t* 
 
 hipError_t launch_decode3d_fixed(const FieldDesc& F, const Params& p, const uint32_t* in32, void* stream)
 {
-  hipStream_t st = S(stream);
+  hipStream_t st = hip_stream(stream);
   switch (p.maxbits / 32) {
     case 2: return launch_dec3d_t<2>(F, p, in32, st);
     case 4: return launch_dec3d_t<4>(F, p, in32, st);

@@ -400,6 +400,16 @@ __device__ __forceinline__ uint64_t window_lds(const uint32_t* rs, uint32_t w0, 
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
+// planes 16..31 below the top of w (bytes 1 and 0 of the same shifted words): the second window
+__device__ __forceinline__ uint64_t window_lds_low(const uint32_t* rs, uint32_t w0, uint32_t w1, uint32_t w2,
+                                                   uint32_t w3)
+{
+  const uint32_t lo = rs[(w0 >> 8) & 255u] | rs[256 + ((w1 >> 8) & 255u)] | rs[512 + ((w2 >> 8) & 255u)] |
+                      rs[768 + ((w3 >> 8) & 255u)];
+  const uint32_t hi = rs[w0 & 255u] | rs[256 + (w1 & 255u)] | rs[512 + (w2 & 255u)] | rs[768 + (w3 & 255u)];
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 // Lean-6 block: the lean-5 stream (encode.c:457-495 for d = 1, fixed rate, kmin = 0) with
 //  * the block maximum as a float max3 of |f| (NaN caught by two unordered compares: it never wins the maximum,
 //    encode.c:146-150, but it casts to INT_MIN, so such blocks take the generic coder);
@@ -408,7 +418,7 @@ __device__ __forceinline__ uint64_t window_lds(const uint32_t* rs, uint32_t w0, 
 //  * the group-phase end jg = clz(u2 | u3) - sh, with 31 for o23 = 0 (jg = M0);
 //  * zero blocks coded by the main path (u = 0 codes to all-zero bits after a zero header), so only tiny-normal and
 //    subnormal maxima (0 < E < 29) take the constant payload.
-template <uint32_t WB>
+template <uint32_t WB, bool W2LOW = false>
 __device__ __forceinline__ uint64_t encode_block1d_lean6(const float* f, const uint32_t* tab, const uint32_t* rs,
                                                          bool& special)
 {
@@ -434,7 +444,8 @@ __device__ __forceinline__ uint64_t encode_block1d_lean6(const float* f, const u
   const uint32_t sh = __builtin_clz(u0 | u1 | o23 | 1u);  // 31 - M0
   const int M0 = 31 - (int)sh;
   const int jg = (int)min(ffbh_hw(o23), 31u) - (int)sh;  // group phase: window nibbles 0 .. jg (o23 = 0: M0)
-  const uint64_t Y = window_lds(rs, u0 << sh, u1 << sh, u2 << sh, u3 << sh);
+  const uint32_t w0 = u0 << sh, w1 = u1 << sh, w2 = u2 << sh, w3 = u3 << sh;
+  const uint64_t Y = window_lds(rs, w0, w1, w2, w3);
   uint32_t pos = 9 + sh;
   uint32_t e = tab[(uint32_t)Y & 255u];
   uint32_t G = e >> 17, gl = (e >> 13) & 15u;
@@ -462,8 +473,13 @@ __device__ __forceinline__ uint64_t encode_block1d_lean6(const float* f, const u
   if (j < 16 && pos < WB) acc |= (Y >> (4 * j)) << pos;  // rest of the window, verbatim
   const uint32_t p2 = pos + 4u * (uint32_t)(16 - j);      // where plane M0 - 16 lands
   if (__any(p2 < WB && M0 >= 16)) {
-    const uint32_t s2 = sh + 16u;  // <= 31 where used (M0 >= 16)
-    const uint64_t Y2 = window_lds(rs, u0 << s2, u1 << s2, u2 << s2, u3 << s2);  // planes M0-16 .. M0-31
+    uint64_t Y2;  // planes M0-16 .. M0-31
+    if constexpr (W2LOW) {
+      Y2 = window_lds_low(rs, w0, w1, w2, w3);
+    } else {
+      const uint32_t s2 = sh + 16u;  // <= 31 where used (M0 >= 16)
+      Y2 = window_lds(rs, u0 << s2, u1 << s2, u2 << s2, u3 << s2);
+    }
     if (p2 < WB && M0 >= 16) acc |= Y2 << p2;
   }
   constexpr uint64_t TINY = tiny_payload_cx((int)WB - 9) << 9;
@@ -542,7 +558,14 @@ __device__ __forceinline__ void pipe_store(uint32_t off, pipe_v4i rs, uint64_t w
 // (vmcnt counts loads and stores together, in issue order). Out-of-range lanes read zeros and their stores are
 // dropped by the buffer range check, so control flow stays wave-uniform. Measured against the persistent grid-stride
 // pipeline above, the one-shot shape streams HBM like a plain copy kernel.
-template <int DT, uint32_t WB, int U, uint32_t T = 256>
+__device__ __forceinline__ uint32_t buf_load_u32(uint32_t off, pipe_v4i rs)
+{
+  uint32_t v;
+  asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+  return v;
+}
+
+template <int DT, uint32_t WB, int U, uint32_t T = 256, int V = 0>
 __global__ __launch_bounds__(T) void k_encode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
                                                          void* __restrict__ out)
 {
@@ -551,13 +574,32 @@ __global__ __launch_bounds__(T) void k_encode_fixed1d_np(const void* __restrict_
   const pipe_v4i rin = buf_rsrc(in, nfull * IB), rout = buf_rsrc(out, nfull * (WB / 8));
   const uint32_t b0 = blockIdx.x * (T * U) + threadIdx.x;
   typename PipeRow<DT>::T r[U];
+  if constexpr ((V & 1) != 0) {
+    // pair-table loads issued first (hand-counted like the data loads), so waiting for them is vmcnt(U) and block 0
+    // can start as soon as its own load lands (a compiler-issued table load after the data loads waits vmcnt(0))
+    static_assert(T == 256, "table fill assumes 256 threads");
+    constexpr int NT = 1280 / 256;
+    const pipe_v4i rt = buf_rsrc(&g_plane_tab5, sizeof(PlaneTab2));
+    uint32_t tv[NT];
 #pragma unroll
-  for (int k = 0; k < U; k++) r[k] = PipeRow<DT>::load((b0 + T * k) * IB, rin);
+    for (int i = 0; i < NT; i++) tv[i] = buf_load_u32((threadIdx.x + 256u * i) * 4u, rt);
 #pragma unroll
-  for (uint32_t t = threadIdx.x; t < 1280; t += T) tab[t] = g_plane_tab5.v[t];
-  // the spread tables are computed, not loaded: entry 256 i + b = byte b reversed onto nibble bit i
+    for (int k = 0; k < U; k++) r[k] = PipeRow<DT>::load((b0 + T * k) * IB, rin);
 #pragma unroll
-  for (uint32_t t = threadIdx.x; t < 1024; t += T) tab[1280 + t] = rspread_entry(t);
+    for (uint32_t t = threadIdx.x; t < 1024; t += T) tab[1280 + t] = rspread_entry(t);
+    asm volatile("s_waitcnt vmcnt(%5)" : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]), "+v"(tv[3]), "+v"(tv[4]) : "n"(U)
+                 : "memory");
+#pragma unroll
+    for (int i = 0; i < NT; i++) tab[threadIdx.x + 256u * i] = tv[i];
+  } else {
+#pragma unroll
+    for (int k = 0; k < U; k++) r[k] = PipeRow<DT>::load((b0 + T * k) * IB, rin);
+#pragma unroll
+    for (uint32_t t = threadIdx.x; t < 1280; t += T) tab[t] = g_plane_tab5.v[t];
+    // the spread tables are computed, not loaded: entry 256 i + b = byte b reversed onto nibble bit i
+#pragma unroll
+    for (uint32_t t = threadIdx.x; t < 1024; t += T) tab[1280 + t] = rspread_entry(t);
+  }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < U; k++) {
@@ -565,7 +607,7 @@ __global__ __launch_bounds__(T) void k_encode_fixed1d_np(const void* __restrict_
     float f[4];
     PipeRow<DT>::unpack(r[k], f);
     bool special;
-    uint64_t w = encode_block1d_lean6<WB>(f, tab, tab + 1280, special);
+    uint64_t w = encode_block1d_lean6<WB, (V & 2) != 0>(f, tab, tab + 1280, special);
     if (special) {
       RegWriter64 rw{0ull, 0u};
       encode_block<1>(rw, f, p);
@@ -619,39 +661,79 @@ __global__ void k_encode_fixed1d_tail(const void* __restrict__ in, uint64_t nval
   else ((uint32_t*)out)[b] = (uint32_t)w;
 }
 
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x)
+{
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t lo = __shfl_up((uint32_t)x, o), hi = __shfl_up((uint32_t)(x >> 32), o);
+    if (lane >= o) x += (uint64_t)lo | ((uint64_t)hi << 32);
+  }
+  return x;
+}
+
 // Exclusive scan of the range totals (one workgroup). base[] gets nranges + 1 entries (last = total bits); the
 // 32-bit words two ranges share are zeroed so both sides can atomicOr into them; the stream's flush word too.
 // d_base (optional): the stream already holds *d_base bits (chunked / appended encode); every offset starts there and
 // the first range ORs its first word into the bits before it.
+// One workgroup: the range totals are read in coalesced chunks of 8192 through LDS (each thread then scans 8
+// consecutive totals; wave prefix by shuffles, 16 wave totals through LDS), so every global access is coalesced --
+// a per-thread walk over its own contiguous slice touched 64 cache lines per wave load (82 us at 32 Ki ranges).
 __global__ __launch_bounds__(1024) void k_scan_ranges(const uint64_t* __restrict__ sums, uint32_t nranges,
                                                       uint64_t* __restrict__ base, uint64_t* __restrict__ total,
                                                       uint32_t* __restrict__ out32, const uint64_t* __restrict__ d_base)
 {
-  __shared__ uint64_t part[1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t per = (nranges + 1023) / 1024;
-  const uint32_t i0 = min(t * per, nranges), i1 = min(i0 + per, nranges);
-  uint64_t s = 0;
-  for (uint32_t i = i0; i < i1; i++) s += sums[i];
-  part[t] = s;
-  __syncthreads();
-  for (uint32_t o = 1; o < 1024; o <<= 1) {
-    uint64_t y = t >= o ? part[t - o] : 0;
+  constexpr uint32_t T = 1024, K = 8, C = T * K;
+  __shared__ uint64_t v[C];
+  __shared__ uint64_t wsum[T / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  uint64_t carry = d_base ? *d_base : 0ull;
+  for (uint32_t c0 = 0; c0 < nranges; c0 += C) {
+    const uint32_t n = min(C, nranges - c0);
+#pragma unroll
+    for (uint32_t k = 0; k < K; k++) {
+      const uint32_t j = t + T * k;
+      v[j] = j < n ? sums[c0 + j] : 0ull;
+    }
     __syncthreads();
-    part[t] += y;
+    uint64_t loc[K], s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < K; k++) {
+      loc[k] = v[t * K + k];
+      s += loc[k];
+    }
+    const uint64_t incl = wave_incl_scan64(s);
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint64_t before = 0, chunk = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < T / 64; w++) {
+      const uint64_t x = wsum[w];
+      before += w < wv ? x : 0ull;
+      chunk += x;
+    }
+    uint64_t run = carry + before + incl - s;
+#pragma unroll
+    for (uint32_t k = 0; k < K; k++) {
+      v[t * K + k] = run;
+      run += loc[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < K; k++) {
+      const uint32_t j = t + T * k;
+      if (j < n) {
+        const uint64_t b = v[j];
+        base[c0 + j] = b;
+        if (c0 + j > 0 && (b & 31)) out32[b >> 5] = 0u;  // a word two ranges share: zeroed for their atomicOr
+      }
+    }
+    carry += chunk;
     __syncthreads();
   }
-  const uint64_t b0 = d_base ? *d_base : 0ull;
-  uint64_t run = b0 + part[t] - s;
-  for (uint32_t i = i0; i < i1; i++) {
-    base[i] = run;
-    if (i > 0 && (run & 31)) out32[run >> 5] = 0u;
-    run += sums[i];
-  }
-  if (t == 1023) {
-    const uint64_t tot = b0 + part[1023];
-    base[nranges] = tot;
-    if (total) *total = tot;
+  if (t == 0) {
+    base[nranges] = carry;
+    if (total) *total = carry;
   }
 }
 
@@ -2061,7 +2143,7 @@ static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, vo
         const uint32_t nc = min(CH, nfull - c0);
         const void* ic = (const char*)in + (size_t)c0 * IB;
         void* oc = (char*)out + (size_t)c0 * (WB / 8);
-        k_encode_fixed1d_np<DT, WB, 8, 256><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
+        k_encode_fixed1d_np<DT, WB, 8, 256, 3><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
       }
     }
   }

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../gcow_amd/csrc/gcow_kernels.hip"
+#include "../../gcow_amd/csrc/gcow_blocks.hip"
 #include "legacy_variants.hip"
 
 namespace gcow {
@@ -892,6 +893,13 @@ extern "C" int ablate_run(int mode, const void* in, uint32_t nfull, void* out, i
     case 61: gcow::k_np5<8><<<(nfull + 2047) / 2048, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 62: gcow::k_chunk5<3><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 63: gcow::k_chunk5<4><<<grid, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    // k_encode_fixed1d_np prologue / second-window variants (V bit 0: table loads first; bit 1: W2 from low bytes)
+    case 100: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64, 8, 256, 0><<<(nfull + 2047) / 2048, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 101: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64, 8, 256, 1><<<(nfull + 2047) / 2048, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 102: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64, 8, 256, 2><<<(nfull + 2047) / 2048, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 103: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64, 8, 256, 3><<<(nfull + 2047) / 2048, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 104: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64, 16, 256, 3><<<(nfull + 4095) / 4096, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
+    case 105: gcow::k_encode_fixed1d_np<gcow::DT_F32, 64, 12, 256, 3><<<(nfull + 3071) / 3072, 256, 0, st>>>(in, nfull, gcow::Params{64, 64, 64, -1074}, out); break;
     case 9: gcow::k_floor1<false><<<(nfull + 255) / 256, 256, 0, st>>>((const float4*)in, nfull, (uint2*)out); break;
     // one-shot, two blocks per lane (16-B store): the access shape a paired-store encoder would have
     case 64: gcow::k_floor2<false><<<(nfull / 2 + 255) / 256, 256, 0, st>>>((const float4*)in, nfull / 2, (uint4*)out); break;

@@ -1,0 +1,177 @@
+// Ablation of the 3-D fixed-rate decoder (not part of libgcow.so): where k_decode3d_fixed's time goes on the C3
+// field (512^3 fp32, rate 8). Modes: 0 and 1 product body, 2 decode only
+// (no scatter: one word per block written), 3 no plane decode (words staged, transform + scatter), 4 stage + scatter
+// only (no decode, no transform).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../gcow_amd/csrc/codec_device.h"
+#include "../../gcow_amd/csrc/field_io.h"
+
+namespace gcow {
+
+// one LDS peek per group test: flag and unary scan from the same 64-bit window
+template <int K, class Rd>
+__device__ __forceinline__ void planes64_v2(Rd& r, int kmin, uint32_t& bits, uint32_t& n, uint32_t* t)
+{
+  if constexpr (K >= 0) {
+    uint64_t x = 0;
+    if (bits && K >= kmin) {
+      const uint32_t m = n < bits ? n : bits;
+      bits -= m;
+      x = r.get(m);
+      while (n < 64u && bits) {
+        const uint64_t w = r.peek64();
+        bits--;
+        if (!(w & 1u)) {
+          r.pos += 1;
+          break;
+        }
+        const uint32_t lim = min(63u - n, bits);
+        const uint64_t ws = w >> 1;
+        const uint32_t z = ws ? (uint32_t)__builtin_ctzll(ws) : 64u;
+        const uint32_t take = z < lim ? z + 1 : lim;
+        r.pos += 1 + take;
+        bits -= take;
+        n += z < lim ? z : lim;
+        x += 1ull << n;
+        n++;
+      }
+    }
+    t[K] = (uint32_t)x;
+    t[32 + K] = (uint32_t)(x >> 32);
+    planes64_v2<K - 1>(r, kmin, bits, n, t);
+  }
+}
+
+// ablation: verbatim reads only (n grows by 8 per plane, no group tests)
+template <int K, class Rd>
+__device__ __forceinline__ void planes64_verb(Rd& r, int kmin, uint32_t& bits, uint32_t& n, uint32_t* t)
+{
+  if constexpr (K >= 0) {
+    uint64_t x = 0;
+    if (bits && K >= kmin) {
+      const uint32_t m = n < bits ? n : bits;
+      bits -= m;
+      x = r.get(m);
+      n = min(64u, n + 8u);
+    }
+    t[K] = (uint32_t)x;
+    t[32 + K] = (uint32_t)(x >> 32);
+    planes64_verb<K - 1>(r, kmin, bits, n, t);
+  }
+}
+
+template <class Rd, int V = 0>
+__device__ __forceinline__ void decode_block_v2(Rd& r, const Params& p, float* f)
+{
+  uint32_t bits = 1;
+  if (r.bit()) {
+    bits += 8;
+    const int emax = (int)r.get(8) - 127;
+    const uint32_t prec = precision(emax, p.maxprec, p.minexp, 3);
+    const uint32_t minb = p.minbits - (p.minbits < bits ? p.minbits : bits);
+    const uint32_t maxb = p.maxbits - bits;
+    uint32_t u[64];
+    const uint32_t budget = exceeded_maxbits(maxb, prec, 64) ? maxb : 0xffffffffu;
+    const int kmin = prec < 32 ? 32 - (int)prec : 0;
+    uint32_t left = budget, n = 0;
+    if constexpr (V == 1) planes64_verb<31>(r, kmin, left, n, u);
+    else planes64_v2<31>(r, kmin, left, n, u);
+    if constexpr (V != 2) {
+      transpose32(u);
+      transpose32(u + 32);
+    }
+    const uint32_t got = budget - left;
+    if (got < minb) r.pos += minb - got;
+    int32_t q[64];
+    inv_reorder<3>(q, u);
+    inv_xform<3>(q);
+    const float s = dequant_scale(emax);
+#pragma unroll
+    for (int i = 0; i < 64; i++) f[i] = s * (float)q[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 64; i++) f[i] = 0.0f;
+    if (p.minbits > bits) r.pos += p.minbits - bits;
+  }
+}
+
+template <uint32_t WPB, int MODE>
+__global__ __launch_bounds__(256) void k_dec3(FieldDesc F, Params p, const uint32_t* __restrict__ in32,
+                                              uint32_t* __restrict__ sink)
+{
+  extern __shared__ uint32_t lds_w[];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * 256u;
+  const uint32_t nvalid = min(256u, F.nblocks - b0);
+  const uint32_t* src = in32 + (uint64_t)b0 * WPB;
+  for (uint32_t j = tid; j < nvalid * WPB; j += 256) lds_w[(j / WPB) * (WPB + 2) + (j % WPB)] = src[j];
+  lds_w[tid * (WPB + 2) + WPB] = 0u;
+  lds_w[tid * (WPB + 2) + WPB + 1] = 0u;
+  __syncthreads();
+  if (tid >= nvalid) return;
+  WordBitReader r{lds_w + tid * (WPB + 2), 0};
+  float f[64];
+  if constexpr (MODE == 5) {
+    decode_block_v2(r, p, f);
+  } else if constexpr (MODE == 6) {
+    decode_block_v2<WordBitReader, 1>(r, p, f);
+  } else if constexpr (MODE == 7) {
+    decode_block_v2<WordBitReader, 2>(r, p, f);
+  } else if constexpr (MODE <= 2) {
+    decode_block<3>(r, p, f);
+  } else if constexpr (MODE == 3) {
+    uint32_t u[64];
+#pragma unroll
+    for (int i = 0; i < 64; i++) u[i] = r.w[i % WPB] * (uint32_t)(i + 1);
+    int32_t q[64];
+    inv_reorder<3>(q, u);
+    inv_xform<3>(q);
+#pragma unroll
+    for (int i = 0; i < 64; i++) f[i] = (float)q[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 64; i++) f[i] = __uint_as_float(r.w[i % WPB] + i);
+  }
+  if constexpr (MODE == 2) {
+    uint32_t h = 0;
+#pragma unroll
+    for (int i = 0; i < 64; i++) h = h * 31u + __float_as_uint(f[i]);
+    sink[b0 + tid] = h;
+  } else {
+    scatter_block<3>(F, b0 + tid, f);
+  }
+}
+
+}  // namespace gcow
+
+extern "C" int dec3_run(int mode, const void* in32, void* out, void* sink, void* stream)
+{
+  gcow::FieldDesc F{};
+  F.data = out;
+  F.n[0] = F.n[1] = F.n[2] = 512; F.n[3] = 1;
+  F.s[0] = 1; F.s[1] = 512; F.s[2] = 512 * 512; F.s[3] = 0;
+  F.bx = F.by = F.bz = 128; F.bw = 1;
+  F.nblocks = 128u * 128u * 128u;
+  F.dims = 3; F.dtype = gcow::DT_F32; F.vec = 1;
+  const gcow::Params p{512, 512, 64, -1074};
+  constexpr uint32_t WPB = 16;
+  const uint32_t g = F.nblocks / 256;
+  const size_t lds = 256 * (WPB + 2) * 4;
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t* i32 = (const uint32_t*)in32;
+  uint32_t* sk = (uint32_t*)sink;
+  switch (mode) {
+    case 0: gcow::k_dec3<WPB, 0><<<g, 256, lds, st>>>(F, p, i32, sk); break;
+    case 1: gcow::k_dec3<WPB, 1><<<g, 256, lds, st>>>(F, p, i32, sk); break;
+    case 2: gcow::k_dec3<WPB, 2><<<g, 256, lds, st>>>(F, p, i32, sk); break;
+    case 3: gcow::k_dec3<WPB, 3><<<g, 256, lds, st>>>(F, p, i32, sk); break;
+    case 4: gcow::k_dec3<WPB, 4><<<g, 256, lds, st>>>(F, p, i32, sk); break;
+    case 5: gcow::k_dec3<WPB, 5><<<g, 256, lds, st>>>(F, p, i32, sk); break;
+    case 6: gcow::k_dec3<WPB, 6><<<g, 256, lds, st>>>(F, p, i32, sk); break;
+    case 7: gcow::k_dec3<WPB, 7><<<g, 256, lds, st>>>(F, p, i32, sk); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
