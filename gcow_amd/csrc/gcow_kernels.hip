@@ -1790,6 +1790,92 @@ __global__ void k_decode_tail1d(FieldDesc F, Params p, const uint64_t* __restric
   scatter_block<1>(F, b, f);
 }
 
+// Many-workgroup form of k_scan_ranges for up to kScanMwMax ranges: workgroup g scans ranges [1024 g, 1024 g + 1024)
+// and finds its starting offset by summing every earlier range total itself (O(n^2 / 2048) loads in all, from L2:
+// 0.5 M loads at 32 Ki ranges), so no second launch, no partials buffer and no inter-workgroup protocol.
+constexpr uint32_t kScanMwMax = 1u << 16;
+
+__global__ __launch_bounds__(256) void k_scan_ranges_mw(const uint64_t* __restrict__ sums, uint32_t nranges,
+                                                        uint64_t* __restrict__ base, uint64_t* __restrict__ total,
+                                                        uint32_t* __restrict__ out32,
+                                                        const uint64_t* __restrict__ d_base)
+{
+  constexpr uint32_t T = 256, K = 4, C = T * K;
+  __shared__ uint64_t v[C];
+  __shared__ uint64_t wsum[T / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t c0 = blockIdx.x * C;
+  const uint32_t n = min(C, nranges - c0);
+#pragma unroll
+  for (uint32_t k = 0; k < K; k++) {
+    const uint32_t j = t + T * k;
+    v[j] = j < n ? sums[c0 + j] : 0ull;
+  }
+  uint64_t pre = 0;  // every earlier range total, 8 loads in flight per thread
+  uint32_t i = t;
+  for (; i + 7 * T < c0; i += 8 * T) {
+    uint64_t a[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) a[k] = sums[i + k * T];
+#pragma unroll
+    for (int k = 0; k < 8; k++) pre += a[k];
+  }
+  for (; i < c0; i += T) pre += sums[i];
+  __syncthreads();
+  uint64_t loc[K], s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < K; k++) {
+    loc[k] = v[t * K + k];
+    s += loc[k];
+  }
+  const uint64_t incl = wave_incl_scan64(s);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)pre, o), hi = __shfl_xor((uint32_t)(pre >> 32), o);
+    pre += (uint64_t)lo | ((uint64_t)hi << 32);
+  }
+  __shared__ uint64_t wpre[T / 64];
+  if (lane == 63) wsum[wv] = incl;
+  if (lane == 0) wpre[wv] = pre;
+  __syncthreads();
+  uint64_t before = 0, chunk = 0, carry = d_base ? *d_base : 0ull;
+#pragma unroll
+  for (uint32_t w = 0; w < T / 64; w++) {
+    before += w < wv ? wsum[w] : 0ull;
+    chunk += wsum[w];
+    carry += wpre[w];
+  }
+  uint64_t run = carry + before + incl - s;
+#pragma unroll
+  for (uint32_t k = 0; k < K; k++) {
+    v[t * K + k] = run;
+    run += loc[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < K; k++) {
+    const uint32_t j = t + T * k;
+    if (j < n) {
+      const uint64_t b = v[j];
+      base[c0 + j] = b;
+      if (c0 + j > 0 && (b & 31)) out32[b >> 5] = 0u;
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1 && t == 0) {
+    base[nranges] = carry + chunk;
+    if (total) *total = carry + chunk;
+  }
+}
+
+static void scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* base, uint64_t* total, uint32_t* out32,
+                        const uint64_t* d_base, hipStream_t st)
+{
+  if (nranges > 4096 && nranges <= kScanMwMax)
+    k_scan_ranges_mw<<<(nranges + 1023) / 1024, 256, 0, st>>>(sums, nranges, base, total, out32, d_base);
+  else
+    k_scan_ranges<<<1, 1024, 0, st>>>(sums, nranges, base, total, out32, d_base);
+}
+
 __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 
 // ------------------------------------------------------------------------------------------------ header stream
@@ -2180,7 +2266,7 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
   const bool var1d = D == 1 && T == 256 && p.minbits <= 1 && p.maxbits >= 160;
   if (var1d) k_count1d_var<DT, 4><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   else k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
-  k_scan_ranges<<<1, 1024, 0, st>>>(ws_sums, plan.nranges, ws_base, d_total, out32, d_base);
+  scan_ranges(ws_sums, plan.nranges, ws_base, d_total, out32, d_base, st);
   if (var1d) {
     // U = 4 blocks per lane (U = 8 measured 0.835 -> 1.083 ms on C5 acc 1e-6: register pressure)
     k_encode1d_var<DT, 4><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_base, out32, index, index_shift);
@@ -2234,7 +2320,7 @@ hipError_t launch_scan_blocks(const uint32_t* lens, uint32_t nblocks, uint64_t* 
                               uint32_t* out32, void* stream)
 {
   k_widen_u32<<<(nblocks + 255) / 256, 256, 0, S(stream)>>>(lens, nblocks, sums);
-  k_scan_ranges<<<1, 1024, 0, S(stream)>>>(sums, nblocks, base, total, out32, nullptr);
+  scan_ranges(sums, nblocks, base, total, out32, nullptr, S(stream));
   return hipGetLastError();
 }
 
@@ -2271,7 +2357,7 @@ hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint
 hipError_t launch_scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* base, uint64_t* total, uint32_t* out32,
                               const uint64_t* d_base, void* stream)
 {
-  k_scan_ranges<<<1, 1024, 0, S(stream)>>>(sums, nranges, base, total, out32, d_base);
+  scan_ranges(sums, nranges, base, total, out32, d_base, S(stream));
   return hipGetLastError();
 }
 

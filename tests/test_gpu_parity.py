@@ -142,6 +142,16 @@ def test_3d_var_oversized_tiles(gc, orc, mode):
     _check_vs_oracle(gc, orc, a, op, index_stride=1)
 
 
+@pytest.mark.parametrize("shape", [(260, 256, 256), (4, 1024, 4100)])
+def test_3d_var_many_tiles(gc, orc, shape):
+    """More than 4096 tiles: the range scan runs as many workgroups (k_scan_ranges_mw), each summing the totals of
+    the ranges before it; the tile count is not a multiple of the workgroup's 1024 ranges."""
+    rng = np.random.default_rng(33)
+    a = (rng.standard_normal(shape) * 1e-2).astype(np.float32)
+    a[:, :, : shape[2] // 3] *= 1e-3
+    _check_vs_oracle(gc, orc, a, orc.accuracy(1e-3), index_stride=1)
+
+
 def test_subnormal_cast_members(gc, orc):
     """Blocks with emax in [-97, -90] whose members are subnormal: the cast must not flush them."""
     rng = np.random.default_rng(5)
