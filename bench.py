@@ -56,10 +56,14 @@ def parse(argv=None):
     ap.add_argument("--rate", type=float, default=16.0)
     ap.add_argument("--values", type=int, default=N_VALUES)
     ap.add_argument("--strong-gib", type=float, default=8.0, help="C4 strong-scaling bucket (GiB of fp32)")
+    ap.add_argument("--c5-values", type=int, default=N_VALUES, help="bf16 values per rank in the c5_sharded leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="only the headline measurement")
     ap.add_argument("--stub", action="store_true",
                     help="harness self-test on CPU: gloo, a trivial step instead of the encode (tests only)")
+    ap.add_argument("--multi-legs", action="store_true",
+                    help="run the N > 1 legs (exchange, subgroups, strong, c5_sharded) even at N = 1, over a one-rank "
+                         "RCCL group (tests: exercises the multi-GPU code on a one-GPU box)")
     return ap.parse_args(argv)
 
 
@@ -91,7 +95,12 @@ class Ctx:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.stub = args.stub
-        if self.world > 1:
+        self.group = self.world > 1 or (args.multi_legs and not args.stub)
+        if self.world == 1 and self.group:
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        if self.group:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if self.stub:
                 dist.init_process_group("gloo")
@@ -587,7 +596,7 @@ def worker(args):
                              "frac_read_write": round((in_bytes + out_bytes) / (sk / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}
 
     if not args.no_extras:
-        if world > 1:
+        if world > 1 or ctx.group:
             extra["encode_allgather"] = leg_c4_exchange(ctx, lambda t: enc(t, stream), x, p, n, out_bytes)
             torch.cuda.empty_cache()
             extra["subgroups"] = leg_subgroups(ctx, p, n)
@@ -595,7 +604,7 @@ def worker(args):
             del x, enc
             torch.cuda.empty_cache()
             extra["strong"] = leg_strong(ctx, p, int(args.strong_gib * (1 << 30)) // 4)
-            extra["c5_sharded"] = leg_c5_sharded(ctx, N_VALUES)
+            extra["c5_sharded"] = leg_c5_sharded(ctx, args.c5_values)
         else:
             extra["host_e2e"] = leg_host_e2e(ctx, lambda t: enc(t, stream), x, p, n, in_bytes, out_bytes)
             extra["configs"] = leg_configs(ctx)
@@ -634,7 +643,7 @@ def worker(args):
         }
         line.update(extra)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if ctx.group:
         dist.destroy_process_group()
 
 

@@ -768,6 +768,7 @@ struct BitReader {
     pos++;
     return b;
   }
+  __device__ __forceinline__ void skip(uint64_t k) { pos += k; }
 };
 
 // Reader over one block's 32-bit words staged in LDS (two zero pad words after the block).
@@ -793,7 +794,9 @@ struct WordBitReader {
     pos++;
     return b;
   }
+  __device__ __forceinline__ void skip(uint64_t k) { pos += k; }
 };
+
 
 // decode_ints (libzfp 0.5.5; sw/src/decode.c:141-183 with block size 4^d). The unary scan of each group test
 // (`for (; n < size - 1 && bits && (bits--, !read_bit()); n++)`) is done with one count-trailing-zeros of the next
@@ -817,11 +820,11 @@ __device__ __forceinline__ uint32_t decode_ints(Rd& r, uint32_t maxbits, uint32_
       const uint64_t w = r.peek64();
       const uint32_t z = w ? (uint32_t)__builtin_ctzll(w) : 64u;
       if (z < lim) {  // zeros, then the one-bit
-        r.pos += z + 1;
+        r.skip(z + 1);
         bits -= z + 1;
         n += z;
       } else {  // scan ran into the last coefficient or the budget: the one is implied
-        r.pos += lim;
+        r.skip(lim);
         bits -= lim;
         n += lim;
       }
@@ -853,11 +856,11 @@ __device__ __forceinline__ void decode_planes64(Rd& r, int kmin, uint32_t& bits,
         const uint64_t w = r.peek64();
         const uint32_t z = w ? (uint32_t)__builtin_ctzll(w) : 64u;
         if (z < lim) {
-          r.pos += z + 1;
+          r.skip(z + 1);
           bits -= z + 1;
           n += z;
         } else {
-          r.pos += lim;
+          r.skip(lim);
           bits -= lim;
           n += lim;
         }
@@ -908,7 +911,7 @@ __device__ __forceinline__ void decode_block(Rd& r, const Params& p, float* f)
     uint32_t got;
     if constexpr (B == 64) got = decode_ints64(r, budget, prec, u);
     else got = decode_ints<B>(r, budget, prec, u);
-    if (got < minb) r.pos += minb - got;
+    if (got < minb) r.skip(minb - got);
     int32_t q[B];
     inv_reorder<D>(q, u);
     inv_xform<D>(q);
@@ -918,7 +921,7 @@ __device__ __forceinline__ void decode_block(Rd& r, const Params& p, float* f)
   } else {
 #pragma unroll
     for (int i = 0; i < B; i++) f[i] = 0.0f;
-    if (p.minbits > bits) r.pos += p.minbits - bits;
+    if (p.minbits > bits) r.skip(p.minbits - bits);
   }
 }
 

@@ -257,3 +257,28 @@ def test_ddp_hooks_world1_bit_exact(gc, orc, nccl_world1, hook, mode):
     want = (np.zeros_like(dec) + dec) / np.float32(1) if hook == "compressed_allgather_hook" else dec
     got = model.weight.grad.reshape(-1).cpu().numpy()
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+# ---------------------------------------------------------------------------------------------- bench N > 1 legs
+def test_bench_multi_legs_world1(gc):
+    """bench.py's multi-GPU legs (C4 exchange with the oracle check of the gathered stream, the sub-communicator
+    curve, strong scaling, C5 sharded with the stitch checked against the oracle) run on the GPU over a one-rank RCCL
+    group (--multi-legs), small sizes: the code the driver's 8-GPU run executes, exercised on a one-GPU box."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--multi-legs", "--steps", "3", "--warmup", "1",
+           "--values", str(1 << 22), "--strong-gib", "0.0625", "--c5-values", str(1 << 22), "--no-cpu-baseline"]
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1
+    assert d["encode_allgather"]["gathered_stream_matches_oracle"] is True
+    assert d["c5_sharded"]["stitched_stream_matches_oracle"] is True
+    assert [c["k"] for c in d["subgroups"]] == [1] and [c["k"] for c in d["strong"]["curve"]] == [1]
