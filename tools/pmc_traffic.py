@@ -21,7 +21,10 @@ def per_launch(path, kernel, counter):
 
 def main():
     kernel, workload, kt, fetch, write, out = sys.argv[1:7]
-    timed = int(sys.argv[7]) if len(sys.argv) > 7 else 0
+    # timed_steps: K (the last K launches) or W:K (launches W+1 .. W+K in issue order: bench.py's timed region when
+    # more launches follow it, e.g. its steady-state block)
+    spec = sys.argv[7] if len(sys.argv) > 7 else "0"
+    skip, timed = (int(v) for v in spec.split(":")) if ":" in spec else (None, int(spec))
     stats = [r for r in csv.DictReader(open(kt + "/kt_kernel_stats.csv"))]
     f_kib, nf = per_launch(fetch + "/pmc_counter_collection.csv", kernel, "FETCH_SIZE")
     w_kib, nw = per_launch(write + "/pmc_counter_collection.csv", kernel, "WRITE_SIZE")
@@ -42,7 +45,8 @@ def main():
     if timed:
         rows = [r for r in csv.DictReader(open(kt + "/kt_kernel_trace.csv")) if kernel in r["Kernel_Name"]]
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-        dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows][-timed:]
+        dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+        dur = dur[-timed:] if skip is None else dur[skip:skip + timed]
         d["timed_region_launches"] = len(dur)
         d["timed_region_avg_duration_ns"] = sum(dur) / len(dur) if dur else None
     json.dump(d, open(out + "_pmc_traffic.json", "w"), indent=1)
