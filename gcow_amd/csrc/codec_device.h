@@ -42,6 +42,14 @@ __device__ __host__ constexpr int perm_index(int D, int i)
 template <int B> struct PlaneType { using T = uint32_t; };
 template <> struct PlaneType<64> { using T = uint64_t; };
 
+// v_ffbh_u32: leading zeros, all ones for 0 (not undefined, unlike __builtin_clz)
+__device__ __forceinline__ uint32_t ffbh_u32(uint32_t x)
+{
+  uint32_t r;
+  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 __device__ __forceinline__ uint64_t lowmask64(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
 
 // ------------------------------------------------------------------------------------------------ stages
@@ -635,25 +643,30 @@ template <int B>
 __device__ __forceinline__ uint32_t encode_ints_length(const uint32_t* u, uint32_t maxprec)
 {
   const int kmin = maxprec < 32 ? 32 - (int)maxprec : 0;
-  const int Llast = u[B - 1] ? 31 - (int)__builtin_clz(u[B - 1]) : -1;
-  // sum_j max(0, R_j - kmin) = sum_j max(R_j, kmin) - B kmin. The last-/first-at-level sums cancel wherever both
-  // neighbours are >= kmin (R is non-increasing), leaving j + 1 at the one j with R_j >= kmin > R_{j+1}: with
-  // c = #{j : R_j >= kmin} they add c, or B - 2 when c = B.
-  int len = 32 - max(kmin, Llast) - B * kmin + max(Llast, kmin) + (Llast >= kmin ? 1 : 0);
-  int c = Llast >= kmin ? 1 : 0;
-  int Rn = Llast;  // R_{j+1}
+  if (kmin >= 32) return 0u;  // no plane is coded
+  // Evaluated through the suffix ORs S_j = u_j | ... | u_{B-1}: R_j = 31 - ffbh(S_j), so with K = 31 - kmin and
+  // z_j = ffbh(S_j) (all ones for S_j = 0): max(R_j, kmin) = 31 - min(z_j, K) (unsigned), R_j >= kmin <=> z_j <= K,
+  // and L_j = R_j <=> u_j holds S_j's leading bit <=> (u_j ^ S_j) < u_j. sum_j max(0, R_j - kmin) = B K - sum min(z_j, K).
+  // The last-/first-at-level sums cancel wherever both neighbours are >= kmin (R is non-increasing), leaving j + 1 at
+  // the one j with R_j >= kmin > R_{j+1}: with c = #{j : R_j >= kmin} they add c, or B - 2 when c = B.
+  const uint32_t K = (uint32_t)(31 - kmin);
+  uint32_t S = u[B - 1];
+  const uint32_t zl = min(ffbh_u32(S), K);  // 31 - max(kmin, L_{B-1})
+  const bool onl = ffbh_u32(S) <= K;
+  // len = 32 - max(kmin, L_{B-1}) + sum_j (max(R_j, kmin) - kmin) + #{j : L_j = R_j >= kmin} + (c or B - 2)
+  uint32_t len = 1u + zl + (uint32_t)B * K - zl + (onl ? 1u : 0u);
+  uint32_t c = onl ? 1u : 0u;
 #pragma unroll
   for (int j = B - 2; j >= 0; j--) {
-    int Lj = u[j] ? 31 - (int)__builtin_clz(u[j]) : -1;
-    asm volatile("" : "+v"(Lj));  // in order: hoisting all 64 leading-plane counts costs 64 VGPRs
-    const int Rj = max(Lj, Rn);
-    const bool on = Rj >= kmin;
-    len += max(Rj, kmin);
-    len += (on && Lj == Rj) ? 1 : 0;
-    c += on ? 1 : 0;
-    Rn = Rj;
+    S |= u[j];
+    uint32_t z = ffbh_u32(S);
+    asm volatile("" : "+v"(z));  // in order: hoisting all 64 leading-plane counts costs 64 VGPRs
+    const bool on = z <= K;
+    len -= min(z, K);
+    len += (on && (u[j] ^ S) < u[j]) ? 1u : 0u;
+    c += on ? 1u : 0u;
   }
-  return (uint32_t)(len + (c == B ? B - 2 : c));
+  return len + (c == (uint32_t)B ? (uint32_t)B - 2u : c);
 }
 
 // encode_block's return value without coding: same header / cast / transform / reorder, then the closed-form length

@@ -854,34 +854,16 @@ __device__ __forceinline__ uint32_t count_block1d_var(const float* f, int minexp
   const int emax = E ? (int)E - 126 : -126;
   const int prec = min((int)maxprec, max(0, emax - minexp + 4));
   if (m == 0 || prec == 0) return 1u;
-  const int kmin = prec < 32 ? 32 - prec : 0;
   const bool tiny = E < 29u;
   const float s = __uint_as_float((283u - (tiny ? 150u : E)) << 23);
   int32_t q[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) q[i] = tiny ? (int32_t)0x80000000 : (int32_t)(f[i] * s);
   fwd_lift(q[0], q[1], q[2], q[3]);
-  int Lv[4], R[4];
+  uint32_t u[4];
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t u = ((uint32_t)q[i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
-    Lv[i] = u ? 31 - (int)__builtin_clz(u) : -1;
-  }
-  R[3] = Lv[3];
-  R[2] = max(Lv[2], R[3]);
-  R[1] = max(Lv[1], R[2]);
-  R[0] = max(Lv[0], R[1]);
-  // the last-/first-at-level terms cancel except across kmin: with c = #{j : R_j >= kmin} they sum to c (c < 4) or 2
-  int len = 9 + 32 - max(kmin, Lv[3]) - 4 * kmin;
-  int c = 0;
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const bool on = R[j] >= kmin;
-    len += max(R[j], kmin);
-    len += (on && Lv[j] == R[j]) ? 1 : 0;
-    c += on ? 1 : 0;
-  }
-  return (uint32_t)(len + (c == 4 ? 2 : c));
+  for (int i = 0; i < 4; i++) u[i] = ((uint32_t)q[i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+  return 9u + encode_ints_length<4>(u, (uint32_t)prec);  // closed form (codec_device.h), prec >= 1 here
 }
 
 // Variable-rate 1-D pass 1: per-range sums of block bit lengths (closed form from the leading planes; generic for

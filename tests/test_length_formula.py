@@ -11,7 +11,34 @@ def _lead(v):
 
 
 def length_formula(u, prec):
-    """Same backward pass as encode_ints_length<B> (codec_device.h)."""
+    """Same backward pass as encode_ints_length<B> (codec_device.h): suffix ORs S_j, z_j = leading zeros of S_j
+    (all ones for 0), K = 31 - kmin."""
+    B = len(u)
+    kmin = 32 - prec if prec < 32 else 0
+    if kmin >= 32:
+        return 0
+    K = 31 - kmin
+
+    def ffbh(v):
+        return 0xFFFFFFFF if v == 0 else 32 - int(v).bit_length()
+
+    S = int(u[B - 1])
+    on = ffbh(S) <= K
+    n = 1 + B * K + (1 if on else 0)
+    c = 1 if on else 0
+    for j in range(B - 2, -1, -1):
+        uj = int(u[j])
+        S |= uj
+        z = ffbh(S)
+        on = z <= K
+        n -= min(z, K)
+        n += 1 if (on and (uj ^ S) < uj) else 0
+        c += 1 if on else 0
+    return n + (B - 2 if c == B else c)
+
+
+def length_leading_planes(u, prec):
+    """The earlier form of the same pass (leading planes L_j and their suffix maxima R_j), kept as a cross-check."""
     B = len(u)
     kmin = 32 - prec if prec < 32 else 0
     last = _lead(u[B - 1])
@@ -70,6 +97,7 @@ def test_length_formula_matches_coder(orc, size):
         _, _, bits = orc.encode_ints(u, 1 << 30, prec, words=words)
         assert length_formula(u, prec) == bits, (u.tolist(), prec)
         assert length_per_plane(u, prec) == bits, (u.tolist(), prec)
+        assert length_leading_planes(u, prec) == bits, (u.tolist(), prec)
 
 
 def test_length_formula_extremes(orc):
