@@ -19,8 +19,8 @@ Extra objects on the same JSON line (they never change `value`):
           against the oracle on sampled ranges of every shard), subgroups (1/2/4/.. ranks over dist.new_group),
           strong (8 GiB split k ways), c5_sharded (bf16 accuracy 1e-6: encode + length exchange + padded all-gather
           + one-launch stitch, checked against the oracle at every shard start)
-  N = 1:  host_e2e (pinned H2D + encode + D2H; PCIe-inclusive), configs (C3 512^3 rate 8 / accuracy 1e-3 encode +
-          decode, C5 bf16 accuracy 1e-6 / 1e-3 device and host path), cpu_baseline (rank 0)
+  N = 1:  host_e2e (pinned H2D + encode + D2H; PCIe-inclusive), configs (C2 rate 8 encode and rate 16 decode, C3 512^3
+          rate 8 / accuracy 1e-3 encode + decode, C5 bf16 accuracy 1e-6 / 1e-3 device and host path), cpu_baseline
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -408,6 +408,27 @@ def leg_configs(ctx):
     compressed bytes)."""
     from gcow_amd import codec
     out = {}
+    # C2 at rate 8 (SURVEY 8(d): rates 16 and 8) and the rate-16 decode (8(f) rank 1), same bucket as the headline
+    n = N_VALUES
+    x = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+    codec.fill_normal(x, 1e-3, seed=SEED, inject=True)
+    st = torch.cuda.current_stream(ctx.dev)
+    enc8 = codec.Encoder((n,), torch.float32, codec.rate(8, 1), ctx.dev)
+    w8, per = timed(ctx, lambda: enc8(x, st), 5, 20, stream=st)
+    k8 = sum(per) / len(per)
+    out["c2_rate8"] = {"ms_per_step": round(w8, 4), "GiBps_input": round(gib(n * 4, w8), 2), "kernel_ms": round(k8, 4),
+                       "encode_roofline": roof(n * 4, n, k8, "k_encode_fixed1d_np<F32, 32>")}
+    del enc8
+    enc16 = codec.Encoder((n,), torch.float32, codec.rate(16, 1), ctx.dev)
+    e16 = enc16(x, st)
+    back = torch.empty_like(x)
+    wd, dper = timed(ctx, lambda: codec.decode(e16, out=back, stream=st), 5, 20, stream=st)
+    dk = sum(dper) / len(dper)
+    out["c2_rate16_decode"] = {"ms_per_step": round(wd, 4), "GiBps_output": round(gib(n * 4, wd), 2),
+                               "kernel_ms": round(dk, 4), "max_abs_err": float((back - x).abs().max()),
+                               "decode_roofline": roof(n * 2, n * 4, dk, "k_decode_fixed1d_np<64, 16>", basis="write")}
+    del enc16, e16, back, x
+    torch.cuda.empty_cache()
     f = _c3_field(ctx.dev)
     nbytes = f.numel() * 4
     for name, p, stride in (("c3_512cube_rate8", codec.rate(8, 3), 0),
