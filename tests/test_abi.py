@@ -110,3 +110,20 @@ def test_bit_stream_roundtrip(L):
     L.stream_rseek(s, 130)
     L.stream_algin_next_word(s)
     assert L.stream_roffset(s) == 192
+
+
+def test_field_of_rejects_expanded_views():
+    """A broadcast / expanded view has stride 0 on a dimension of size > 1; the ABI reads a 0 stride as "dense"
+    (sw/src/zfp.c:37-38), so passing it through would read past the tensor's storage: field_of refuses it,
+    and accepts the same data once contiguous, and size-1 dimensions with any stride."""
+    torch = pytest.importorskip("torch")
+    from gcow_amd import codec
+    base = torch.arange(16, dtype=torch.float32)
+    with pytest.raises(codec.GcowError):
+        codec.field_of(base.view(1, 16).expand(8, 16))
+    with pytest.raises(codec.GcowError):
+        codec.field_of(base[:1].expand(64))
+    f = codec.field_of(base.view(1, 16).expand(8, 16).contiguous())
+    assert (f.nx, f.ny, f.sx, f.sy) == (16, 8, 1, 16)
+    g = codec.field_of(base.view(16, 1))  # size-1 dimension: its stride never matters
+    assert (g.nx, g.ny) == (1, 16)
