@@ -144,19 +144,21 @@ __global__ __launch_bounds__(256) void k_dec3(FieldDesc F, Params p, const uint3
                                               uint32_t* __restrict__ sink)
 {
   extern __shared__ uint32_t lds_w[];
+  constexpr uint32_t SW = MODE == 10 ? WPB + 3 : WPB + 2;  // words per block in LDS
   const uint32_t tid = threadIdx.x;
   const uint32_t b0 = blockIdx.x * 256u;
   const uint32_t nvalid = min(256u, F.nblocks - b0);
   const uint32_t* src = in32 + (uint64_t)b0 * WPB;
-  for (uint32_t j = tid; j < nvalid * WPB; j += 256) lds_w[(j / WPB) * (WPB + 2) + (j % WPB)] = src[j];
-  lds_w[tid * (WPB + 2) + WPB] = 0u;
-  lds_w[tid * (WPB + 2) + WPB + 1] = 0u;
+  for (uint32_t j = tid; j < nvalid * WPB; j += 256) lds_w[(j / WPB) * SW + (j % WPB)] = src[j];
+  for (uint32_t k = WPB; k < SW; k++) lds_w[tid * SW + k] = 0u;
   __syncthreads();
   if (tid >= nvalid) return;
   // mode 8: every lane of a wave decodes the wave's first block (the same work without divergence)
-  WordBitReader r{lds_w + (MODE == 8 ? (tid & ~63u) : tid) * (WPB + 2), 0};
+  WordBitReader r{lds_w + (MODE == 8 ? (tid & ~63u) : tid) * SW, 0};
   float f[64];
-  if constexpr (MODE == 9) {
+  if constexpr (MODE == 10) {
+    decode_block<3>(r, p, f);
+  } else if constexpr (MODE == 9) {
     WinReader rw(lds_w + tid * (WPB + 2), 0);
     decode_block<3>(rw, p, f);
   } else if constexpr (MODE == 8) {
@@ -221,6 +223,7 @@ extern "C" int dec3_run(int mode, const void* in32, void* out, void* sink, void*
     case 7: gcow::k_dec3<WPB, 7><<<g, 256, lds, st>>>(F, p, i32, sk); break;
     case 8: gcow::k_dec3<WPB, 8><<<g, 256, lds, st>>>(F, p, i32, sk); break;
     case 9: gcow::k_dec3<WPB, 9><<<g, 256, lds, st>>>(F, p, i32, sk); break;
+    case 10: gcow::k_dec3<WPB, 10><<<g, 256, lds + 256 * 4, st>>>(F, p, i32, sk); break;
     default: return -1;
   }
   return (int)hipGetLastError();
