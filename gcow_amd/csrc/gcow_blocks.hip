@@ -171,8 +171,12 @@ __global__ __launch_bounds__(64) void k_encode3d_var(FieldDesc F, Params p, cons
 
 // The matching decoder: the workgroup stages its 256 blocks' stream words in LDS (coalesced), each lane decodes its
 // block from LDS (libzfp decode semantics) and scatters it.
+// Bounded to 6 waves per SIMD (101 -> 80 VGPRs, 30 spilled to scratch): the decoder is VALU-bound with divergent
+// group-test loops, and the extra waves hide more of it than the spills cost (C3 rate 8 decode 0.337 -> 0.297 ms,
+// tools/bench_configs.py c3).
 template <uint32_t WPB>
-__global__ __launch_bounds__(256) void k_decode3d_fixed(FieldDesc F, Params p, const uint32_t* __restrict__ in32)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_decode3d_fixed(
+    FieldDesc F, Params p, const uint32_t* __restrict__ in32)
 {
   extern __shared__ uint32_t lds_w[];  // 256 x (WPB + 2) words: the block, then two zero pad words for peek64
   const uint32_t tid = threadIdx.x;
