@@ -27,7 +27,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import platform
 import socket
@@ -76,11 +75,12 @@ def _free_port() -> int:
     return p
 
 
-def launch(args) -> int:
-    """N > 1 without a torchrun environment: start N ranks (one process per GPU) through torchrun on 127.0.0.1 and
-    return its exit code. Called before anything initialises HIP in this process."""
+def launch(args, argv) -> int:
+    """N > 1 without a torchrun environment: start N ranks (one process per GPU) through torchrun on 127.0.0.1, each
+    with the argument list this process was given (`argv`), and return its exit code. Called before anything
+    initialises HIP in this process."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
-           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + list(argv)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env["GCOW_BENCH_LAUNCHER"] = "self"
@@ -392,17 +392,6 @@ def leg_host_e2e(ctx, enc, x, p, n, in_bytes, out_bytes):
                     "H2D / encode / D2H on three streams (codec.HostEncoder)"}
 
 
-def _c3_field(dev, side=512):
-    """f = sin(6 pi x) cos(4 pi y) sin(2 pi z) + 1e-3 N(0, 1) on the [0, 1)^3 grid (z slowest)."""
-    g = torch.arange(side, device=dev, dtype=torch.float32) / side
-    f = (torch.sin(6 * math.pi * g)[None, None, :] * torch.cos(4 * math.pi * g)[None, :, None] *
-         torch.sin(2 * math.pi * g)[:, None, None])
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(SEED)
-    f += 1e-3 * torch.randn(f.shape, device=dev, generator=gen)
-    return f.contiguous()
-
-
 def leg_configs(ctx):
     """C3 and C5 at N = 1, each with its own roofline fraction (read-only bytes = the input; read + write adds the
     compressed bytes)."""
@@ -429,7 +418,7 @@ def leg_configs(ctx):
                                "decode_roofline": roof(n * 2, n * 4, dk, "k_decode_fixed1d_np<64, 16>", basis="write")}
     del enc16, e16, back, x
     torch.cuda.empty_cache()
-    f = _c3_field(ctx.dev)
+    f = codec.c3_field(ctx.dev)  # the field tests/test_gpu_parity.py::test_c3_full_size_roundtrip checks
     nbytes = f.numel() * 4
     for name, p, stride in (("c3_512cube_rate8", codec.rate(8, 3), 0),
                             ("c3_512cube_acc1e-3", codec.accuracy(1e-3), 1)):
@@ -491,23 +480,38 @@ def _cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline(x: torch.Tensor, rate: float) -> dict:
-    """The reference's CPU path on this host's cores, on bounded samples of the same bucket, best of 5:
-      reference  sw/ zfp_compress compiled from /root/reference/sw/src (oracle/_ref, g++ -O3 -march=x86-64-v3), one
-                 thread (sw/ has no threads), 2-D (its only layout: sw/src/zfp.c:12-24) on 64 Mi values viewed 8192^2;
-      port_1t    the oracle restatement (gcc -O3 -march=native, built here) on the same 1-D rate-16 config, 1 thread,
-                 32 Mi values;
-      port_mt    the same on the whole 256 Mi bucket with T threads over block-aligned shards + a serial bit stitch.
+def _cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cpu.max), or None when unlimited / unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(x: torch.Tensor, rate: float, dev) -> dict:
+    """The reference's CPU path on this host's cores, best of N, encode only, host-resident:
+      reference        sw/ zfp_compress compiled from /root/reference/sw/src (oracle/_ref, g++ -O3), one thread (sw/
+                       has no threads), 2-D (its only layout: sw/src/zfp.c:12-24) on the WHOLE 256 Mi bucket viewed as
+                       16384 x 16384, fixed rate `rate` (2-D minbits = maxbits = 16 rate);
+      port_1t          the oracle restatement (gcc -O3 -march=native, built here) on the C2 config (1-D rate `rate`),
+                       1 thread, the bucket's first 32 Mi values;
+      port_mt          the same on the whole bucket with T = len(sched_getaffinity) threads over block-aligned shards +
+                       a serial bit stitch (port_mt_omp: T = OMP_NUM_THREADS, the box's CPU share);
+      c3_*, c5_*       the restatement on the C3 field (512^3, 3-D rate 8 / accuracy 1e-3; the sw/ reference has no
+                       3-D) and the C5 bucket (256 Mi bf16, accuracy 1e-6; no bf16 in sw/): T threads on the whole
+                       input, 1 thread on a bounded slice.
     The headline is `reference`; without oracle/_ref it is port_1t and `reference_missing` says why."""
     import ctypes as C
 
     import numpy as np
 
+    from gcow_amd import codec
     from oracle import oracle as O
     a = x.detach().cpu().numpy()
     legs = {}
 
-    def best(fn, reps=5):
+    def best(fn, reps):
         ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
@@ -515,18 +519,25 @@ def cpu_baseline(x: torch.Tensor, rate: float) -> dict:
             ts.append(time.perf_counter() - t0)
         return min(ts)
 
+    def leg(name, nbytes, dt, cores, sample, reps):
+        legs[name] = {"value": round(nbytes / dt / 2 ** 30, 4), "unit": "GiB/s of uncompressed input", "cores": cores,
+                      "seconds_best": round(dt, 4), "best_of": reps, "sample": sample}
+
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS") or 0) or None
     R = O.ref()
     missing = None
     if R is not None:
-        side = 8192
-        a2 = np.ascontiguousarray(a[: side * side].reshape(side, side))
+        side = 16384
+        a2 = a[: side * side].reshape(side, side)
+        assert a2.flags.c_contiguous
         p = O.rate(rate, 2)
         out = np.zeros(O.max_words(a2.shape, p) + 4, np.uint64)
         dt = best(lambda: R.gcow_ref_compress_2d(a2.ctypes.data_as(C.POINTER(C.c_float)), side, side, *p.tuple(),
-                                                   out.ctypes.data_as(C.POINTER(C.c_uint64)), out.nbytes))
-        legs["reference"] = {"value": round(a2.nbytes / dt / 2 ** 30, 4), "cores": 1, "seconds_best": round(dt, 3),
-                             "sample": "sw/ zfp_compress, 8192 x 8192 fp32 view of the bucket's first 64 Mi values, "
-                                       "fixed rate %g (2-D: minbits = maxbits = %d), 1 thread" % (rate, p.maxbits)}
+                                                   out.ctypes.data_as(C.POINTER(C.c_uint64)), out.nbytes), 3)
+        leg("reference", a2.nbytes, dt, 1, "sw/ zfp_compress on the whole 256 Mi-value bucket viewed as 16384 x 16384 "
+            "fp32, fixed rate %g (2-D: minbits = maxbits = %d), 1 thread" % (rate, p.maxbits), 3)
+        del out
     else:
         missing = ("oracle/_ref/libgcow_ref.so absent: it is compiled from /root/reference/sw/src by oracle/Makefile "
                    "(make -C oracle ref) in the build container and travels with the tree")
@@ -534,19 +545,37 @@ def cpu_baseline(x: torch.Tensor, rate: float) -> dict:
     L, flags = O.native_lib()
     p1 = O.rate(rate, 1)
     s1 = np.ascontiguousarray(a[: 32 << 20])
-    dt = best(lambda: O.compress(s1, p1, L=L))
-    legs["port_1t"] = {"value": round(s1.nbytes / dt / 2 ** 30, 4), "cores": 1, "seconds_best": round(dt, 3),
-                       "sample": "oracle restatement (%s), 1-D fixed rate %g, first 32 Mi values" % (flags, rate)}
-    T = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
-    T = max(1, min(T, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else T))
-    dt = best(lambda: O.compress(a, p1, threads=T, L=L))
-    legs["port_mt"] = {"value": round(a.nbytes / dt / 2 ** 30, 4), "cores": T, "seconds_best": round(dt, 3),
-                       "sample": "oracle restatement (%s), 1-D fixed rate %g, whole 256 Mi bucket, %d threads over "
-                                 "block-aligned shards + serial bit stitch" % (flags, rate, T)}
+    leg("port_1t", s1.nbytes, best(lambda: O.compress(s1, p1, L=L), 5), 1,
+        "oracle restatement (%s), 1-D fixed rate %g, first 32 Mi values" % (flags, rate), 5)
+    leg("port_mt", a.nbytes, best(lambda: O.compress(a, p1, threads=aff, L=L), 5), aff,
+        "oracle restatement (%s), 1-D fixed rate %g, whole 256 Mi bucket, %d threads (sched_getaffinity) over "
+        "block-aligned shards + serial bit stitch" % (flags, rate, aff), 5)
+    if omp and omp != aff:
+        leg("port_mt_omp", a.nbytes, best(lambda: O.compress(a, p1, threads=omp, L=L), 5), omp,
+            "as port_mt with T = OMP_NUM_THREADS = %d (the box's CPU share)" % omp, 5)
+    del s1
+    # C3: the 512^3 field the GPU configs leg times
+    f = codec.c3_field(dev).cpu().numpy()
+    slab = np.ascontiguousarray(f[:64])
+    for name, op in (("c3_rate8", O.rate(8, 3)), ("c3_acc1e-3", O.accuracy(1e-3))):
+        leg(name + "_port_mt", f.nbytes, best(lambda: O.compress(f, op, threads=aff, L=L), 3), aff,
+            "oracle restatement, 3-D %s, the whole 512^3 C3 field, %d threads" % (name[3:], aff), 3)
+        leg(name + "_port_1t", slab.nbytes, best(lambda: O.compress(slab, op, L=L), 3), 1,
+            "oracle restatement, 3-D %s, 64 z-planes (512 x 512 x 64) of the C3 field, 1 thread" % name[3:], 3)
+    del f, slab
+    # C5: the bf16 bucket (exact widening, accuracy 1e-6)
+    hb = x.to(torch.bfloat16).cpu().view(torch.int16).numpy().view(np.uint16)
+    op = O.accuracy(1e-6)
+    leg("c5_bf16_acc1e-6_port_mt", hb.nbytes, best(lambda: O.compress(hb, op, threads=aff, L=L), 3), aff,
+        "oracle restatement, 1-D bf16 accuracy 1e-6, the whole 256 Mi-value C5 bucket, %d threads" % aff, 3)
+    h1 = np.ascontiguousarray(hb[: 32 << 20])
+    leg("c5_bf16_acc1e-6_port_1t", h1.nbytes, best(lambda: O.compress(h1, op, L=L), 3), 1,
+        "oracle restatement, 1-D bf16 accuracy 1e-6, first 32 Mi values of the C5 bucket, 1 thread", 3)
     head = legs.get("reference") or legs["port_1t"]
     d = {"value": head["value"], "unit": "GiB/s", "cores": head["cores"],
          "kind": "reference" if "reference" in legs else "port", "sample": head["sample"],
-         "cpu": _cpu_model(), "host_cpus": os.cpu_count(), "best_of": 5, "legs": legs}
+         "cpu": _cpu_model(), "host_cpus": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": omp,
+         "cgroup_cpu_quota": _cpu_quota(), "legs": legs}
     if missing:
         d["reference_missing"] = missing
     return d
@@ -601,6 +630,22 @@ def worker(args):
     roofline["traffic"] = traffic
     roofline["traffic_source"] = (src + " (rocprofv3 --pmc TCC read + write bytes per launch, same kernel and "
                                   "workload; not measured in this run)") if src else None
+    if p.maxbits in (32, 64):
+        # measured device-copy ceiling of the encoder's own access pattern (BASELINE.md:59): the same grid, loads and
+        # stores without the coding (k_copy_pattern1d), same protocol, right after the headline
+        cp_out = torch.empty(n // 4 * p.maxbits // 64 + 1, dtype=torch.int64, device=ctx.dev)
+        _, cper = timed(ctx, lambda: codec.copy_pattern(x, cp_out, p.maxbits, stream), args.warmup, args.steps,
+                        stream=stream)
+        ck = ctx.max_over_ranks([sum(cper) / len(cper)])[0]
+        roofline["copy_ceiling"] = {
+            "kernel": "k_copy_pattern1d", "kernel_ms": round(ck, 5),
+            "achieved": round(in_bytes / (ck / 1e3) / 1e9, 1), "unit": "GB/s (uncompressed bytes read)",
+            "frac": round(in_bytes / (ck / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "frac_read_write": round((in_bytes + out_bytes) / (ck / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "encoder_frac_of_ceiling": round(ck / kern_ms, 4),
+            "note": "the encoder's grid, 16-B loads and %d-bit stores per block with no coding: the HBM floor of "
+                    "this access pattern (--warmup/--steps as the headline)" % p.maxbits}
+        del cp_out
     extra = {"per_launch_ms": {"first": round(per[0], 4), "median": round(statistics.median(per), 4),
                                "min": round(min(per), 4), "max": round(max(per), 4)}}
     # the same kernel once the clock has settled under load (>= 0.25 s of back-to-back launches)
@@ -636,7 +681,7 @@ def worker(args):
             if "x" not in locals():
                 x = torch.empty(n, dtype=torch.float32, device=ctx.dev)
                 codec.fill_normal(x, 1e-3, seed=SEED, inject=True)
-            cpu = cpu_baseline(x, args.rate)
+            cpu = cpu_baseline(x, args.rate, ctx.dev)
         except Exception as ex:  # the GPU measurement stands on its own
             cpu = {"error": repr(ex)}
             print("bench.py: cpu_baseline failed: %r" % (ex,), file=sys.stderr)
@@ -669,9 +714,10 @@ def worker(args):
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch(args))
+        sys.exit(launch(args, argv))
     worker(args)
 
 

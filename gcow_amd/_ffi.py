@@ -106,7 +106,7 @@ def load():
         "gcow_decode_device": (i32, [pi, pp, vp, sz, vp, u32, vp]),
         "gcow_stitch_device": (i32, [vp, u64, vp, u64, vp]),
         "gcow_stitch_shards_device": (i32, [vp, u64, vp, u64, vp, u32, vp]),
-        "gcow_decode_mean_device": (i32, [pi, pp, vp, u64, u32, vp, u64, u32, vp]),
+        "gcow_decode_mean_device": (i32, [pi, pp, vp, sz, u64, u32, vp, u64, u32, vp]),
         "gcow_header_bits": (C.c_uint, [pp]),
         "gcow_write_header": (C.c_uint, [pi, pp, P(u64)]),
         "gcow_read_header": (C.c_uint, [P(u64), sz, pi, pp]),
@@ -114,6 +114,7 @@ def load():
         "gcow_encode_device_zfp": (i32, [pi, pp, vp, sz, vp, vp, sz, vp]),
         "gcow_decode_device_at": (i32, [pi, pp, vp, sz, u64, vp, u32, vp]),
         "gcow_fill_normal_device": (i32, [vp, sz, C.c_double, u64, i32, vp]),
+        "gcow_copy_pattern_device": (i32, [vp, i32, sz, u32, vp, vp]),
         "gcow_stage_emax_device": (i32, [vp, u32, u32, vp, vp]),
         "gcow_stage_cast_device": (i32, [vp, vp, u32, u32, vp, vp]),
         "gcow_stage_xform_device": (i32, [vp, u32, u32, i32, vp]),

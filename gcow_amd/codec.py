@@ -230,12 +230,11 @@ def decode_mean(streams: torch.Tensor, stream_words: int, nstreams: int, n: int,
                 out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
     """Mean of the decodes of nstreams 1-D streams of n values (stream r at streams[r * stream_words:], 2 readable
     words after the last one), accumulated in rank order in fp32 (gcow_decode_mean_device): one launch."""
-    if streams.numel() < nstreams * stream_words + 2:
-        raise GcowError("decode_mean: the stream buffer needs 2 words of padding after the last stream")
     if out is None:
         out = torch.empty(n, dtype=torch.float32, device=streams.device)
     f = field_of(out)
-    check(load().gcow_decode_mean_device(C.byref(f), C.byref(params), streams.data_ptr(), stream_words, nstreams,
+    check(load().gcow_decode_mean_device(C.byref(f), C.byref(params), streams.data_ptr(), streams.numel() * 8,
+                                         stream_words, nstreams,
                                          index.data_ptr() if index is not None else None, index_words, index_stride,
                                          _stream_ptr(stream)), "gcow_decode_mean_device")
     return out
@@ -247,6 +246,34 @@ def fill_normal(out: torch.Tensor, sigma: float = 1e-3, seed: int = 0x67636F77, 
     check(load().gcow_fill_normal_device(out.data_ptr(), out.numel(), sigma, seed, int(inject),
                                          _stream_ptr(stream)), "gcow_fill_normal_device")
     return out
+
+
+def copy_pattern(x: torch.Tensor, out: torch.Tensor, bits_per_block: int = 64, stream=None):
+    """The fixed-rate 1-D encoder's memory access pattern without coding (gcow_copy_pattern_device): the HBM floor
+    of that kernel, for bench.py's roofline.copy_ceiling."""
+    dt = DTYPE_BF16 if x.dtype == torch.bfloat16 else DTYPE_FLOAT
+    if not (x.is_cuda and x.is_contiguous()) or out.numel() * out.element_size() * 8 < x.numel() // 4 * bits_per_block:
+        raise GcowError("copy_pattern: contiguous device input and an output of nblocks * bits_per_block bits")
+    check(load().gcow_copy_pattern_device(x.data_ptr(), dt, x.numel(), bits_per_block, out.data_ptr(),
+                                          _stream_ptr(stream)), "gcow_copy_pattern_device")
+    return out
+
+
+def c3_field(device=None, side: int = 512, seed: int = 21) -> torch.Tensor:
+    """SURVEY 8(d) C3 volume on the device: f = sin(6 pi x) cos(4 pi y) sin(2 pi z) + 1e-3 N(0, 1) on the [0, 1)^3
+    grid (z slowest), the noise from fill_normal. The bench times this field and the full-size parity test checks the
+    same one (copied to the host) against the oracle."""
+    import math as _m
+    dev = torch.device(device or "cuda")
+    g = torch.arange(side, device=dev, dtype=torch.float64) / side
+    sx = torch.sin(6 * _m.pi * g).float()
+    cy = torch.cos(4 * _m.pi * g).float()
+    sz = torch.sin(2 * _m.pi * g).float()
+    f = torch.empty(side ** 3, dtype=torch.float32, device=dev)
+    fill_normal(f, 1.0, seed=seed, inject=False)
+    f = f.view(side, side, side).mul_(1e-3)
+    f += sx[None, None, :] * cy[None, :, None] * sz[:, None, None]
+    return f.contiguous()
 
 
 # ------------------------------------------------------------------------------------------- zfpy byte streams

@@ -278,7 +278,7 @@ struct OutState {
   size_t d_index_cap = 0;
   void* d_ws = nullptr;
   size_t d_ws_cap = 0;
-  uint64_t* d_u64 = nullptr;  // [0] total bits, [1] end position
+  uint64_t* d_u64 = nullptr;  // [0] total bits, [1] end position, [2] stream-compare flag
   // what the cached device stream holds
   bool valid = false;
   const void* host_begin = nullptr;
@@ -288,7 +288,7 @@ struct OutState {
   uint32_t dims = 0;
   uint64_t nblocks = 0;
   uint64_t words = 0;
-  uint64_t fp[64] = {};  // fingerprint() of the caller's stream when the cache was filled
+  uint64_t hash = 0;  // hash_words() of the caller's host stream when the cache was filled
 };
 
 std::mutex g_mu;
@@ -354,23 +354,20 @@ void field_span(const zfp_input* in, ptrdiff_t* lo, ptrdiff_t* hi)
 
 bool strided(const zfp_input* in) { return in->sx || in->sy || in->sz || in->sw; }
 
-// Sampled fingerprint of a stream's first `words` words (host or device): the first, the last and 62 evenly spaced
-// words. zfp_decompress reuses the device copy left by zfp_compress only while this still matches, so a caller that
-// rewrote the host buffer in between (read another stream into it, say) is decoded from its new contents.
-constexpr int kFingerprint = 64;
-bool fingerprint(const uint64_t* w, uint64_t words, bool dev, uint64_t* fp)
+// Whole-stream check that the caller's buffer still holds the stream zfp_compress left in it (zfp_decompress reuses
+// the device copy only then; a caller that rewrote its buffer -- another stream of the same shape, a local edit -- is
+// decoded from its new contents). Host streams: a 64-bit hash of every word, taken at compress time and recomputed
+// at decompress time. Device streams: every word compared on the device against the cached copy.
+uint64_t hash_words(const uint64_t* w, uint64_t words)
 {
-  std::memset(fp, 0, kFingerprint * 8);
-  if (!words) return true;
-  const uint64_t step = words > 1 ? std::max<uint64_t>((words - 1) / (kFingerprint - 1), 1) : 1;
-  const uint64_t cnt = std::min<uint64_t>(words > 1 ? (words - 1) / step + 1 : 1, kFingerprint - 1);
-  if (!dev) {
-    for (uint64_t i = 0; i < cnt; i++) fp[i] = w[i * step];
-    fp[kFingerprint - 1] = w[words - 1];
-    return true;
+  uint64_t h = 0x67636F77ull ^ (words * 0x9E3779B97F4A7C15ull);
+  for (uint64_t i = 0; i < words; i++) {
+    uint64_t z = w[i] + 0x9E3779B97F4A7C15ull * (i + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    h = (h ^ z ^ (z >> 31)) * 0xff51afd7ed558ccdull;
   }
-  if (hipMemcpy2D(fp, 8, w, step * 8, 8, cnt, hipMemcpyDeviceToHost) != hipSuccess) return false;
-  return hipMemcpy(fp + kFingerprint - 1, w + words - 1, 8, hipMemcpyDeviceToHost) == hipSuccess;
+  return h ^ (h >> 33);
 }
 
 // Host-side copy of `bits` bits from words src into stream s at its current write position (stream.c:61-92).
@@ -978,8 +975,9 @@ gcow_status gcow_stitch_shards_device(uint64_t* d_dst, uint64_t dst_words, const
 }
 
 gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p, const uint64_t* d_streams,
-                                    uint64_t stream_words, uint32_t nstreams, const uint64_t* d_index,
-                                    uint64_t index_words, uint32_t index_stride, void* hip_stream)
+                                    size_t streams_bytes, uint64_t stream_words, uint32_t nstreams,
+                                    const uint64_t* d_index, uint64_t index_words, uint32_t index_stride,
+                                    void* hip_stream)
 {
   gcow::FieldDesc F;
   gcow_status st = make_field(field, F, true);
@@ -987,15 +985,31 @@ gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p
   if ((st = check_params(p, 1))) return st;
   if (F.dims != 1) return fail(GCOW_ERR_UNSUPPORTED, "decode_mean is for 1-D buckets");
   if (!nstreams || !d_streams) return fail(GCOW_ERR_INVALID, "no streams");
+  // the decoders read up to two words past a stream's last bit (64-bit windows): the buffer holds them
+  if (streams_bytes / 8 < (uint64_t)nstreams * stream_words + 2)
+    return fail(GCOW_ERR_INVALID, "stream buffer smaller than nstreams * stream_words + 2 words");
   if (p->minbits != p->maxbits) {
-    if (!(p->minbits <= 1 && p->maxbits >= 160))
-      return fail(GCOW_ERR_UNSUPPORTED, "variable-rate decode_mean needs minbits <= 1, maxbits >= 160");
     if (!d_index || index_stride != 16 || index_words < (F.nblocks + 15) / 16)
       return fail(GCOW_ERR_INVALID, "variable-rate decode_mean needs each stream's index (stride 16)");
-  } else if (stream_words < ((uint64_t)F.nblocks * p->maxbits + 63) / 64) {
-    return fail(GCOW_ERR_INVALID, "stream_words below one fixed-rate stream");
+  } else {
+    if (d_index || index_stride || index_words)
+      return fail(GCOW_ERR_INVALID, "fixed-rate decode_mean takes no block index (blocks are at b * maxbits)");
+    if (stream_words < ((uint64_t)F.nblocks * p->maxbits + 63) / 64)
+      return fail(GCOW_ERR_INVALID, "stream_words below one fixed-rate stream");
   }
   GCOW_HIP(gcow::launch_decode_mean1d(F, P(*p), d_streams, stream_words, nstreams, d_index, index_words, hip_stream));
+  return GCOW_OK;
+}
+
+gcow_status gcow_copy_pattern_device(const void* d_in, int dtype, size_t nvals, uint32_t out_bits_per_block,
+                                     void* d_out, void* hip_stream)
+{
+  if ((!d_in || !d_out) && nvals >= 4) return fail(GCOW_ERR_INVALID, "null buffer");
+  if (dtype != dtype_float && dtype != dtype_bf16) return fail(GCOW_ERR_UNSUPPORTED, "dtype_float or dtype_bf16");
+  if (out_bits_per_block != 32 && out_bits_per_block != 64) return fail(GCOW_ERR_INVALID, "32 or 64 bits per block");
+  if (nvals / 4 >= (1ull << 32)) return fail(GCOW_ERR_UNSUPPORTED, "more than 2^32 blocks per call");
+  GCOW_HIP(gcow::launch_copy_pattern1d(d_in, dtype == dtype_bf16 ? gcow::DT_BF16 : gcow::DT_F32, nvals,
+                                       out_bits_per_block, d_out, hip_stream));
   return GCOW_OK;
 }
 
@@ -1092,7 +1106,7 @@ size_t zfp_compress(zfp_output* output, const zfp_input* input)
   if (grow(&st->d_stream, &st->d_stream_cap, cap) != hipSuccess ||
       grow((void**)&st->d_index, &st->d_index_cap, (nidx + 1) * 8) != hipSuccess ||
       grow(&st->d_ws, &st->d_ws_cap, ws + 8) != hipSuccess ||
-      (!st->d_u64 && hipMalloc((void**)&st->d_u64, 16) != hipSuccess)) {
+      (!st->d_u64 && hipMalloc((void**)&st->d_u64, 24) != hipSuccess)) {
     g_err = "device allocation failed";
     return 0;
   }
@@ -1136,7 +1150,7 @@ size_t zfp_compress(zfp_output* output, const zfp_input* input)
     free(tmp);
     stream_flush(s);
   }
-  if (!fingerprint((const uint64_t*)s->begin, words, dev_out, st->fp)) return 0;
+  st->hash = dev_out ? 0 : hash_words((const uint64_t*)s->begin, words);
   st->valid = true;
   st->host_begin = s->begin;
   st->words = words;
@@ -1171,12 +1185,21 @@ size_t zfp_decompress(zfp_output* output, const zfp_input* input)
   const bool fixed = p.minbits == p.maxbits;
   bool cached = st->valid && start == 0 && st->host_begin == s->begin && st->dims == d &&
                 st->nblocks == F.nblocks && std::memcmp(&st->params, &p, sizeof(p)) == 0;
-  if (cached) {  // the caller may have rewritten its buffer since zfp_compress filled the cache
-    uint64_t fp[kFingerprint];
-    cached = fingerprint((const uint64_t*)s->begin, st->words, dev_stream, fp) &&
-             std::memcmp(fp, st->fp, sizeof(fp)) == 0;
+  // the buffer must still hold the whole cached stream (a smaller buffer at the same address is not read past its end)
+  if (cached && s->end > 0 && (uint64_t)s->end < st->words) cached = false;
+  if (!st->d_u64 && hipMalloc((void**)&st->d_u64, 24) != hipSuccess) return 0;
+  if (cached) {  // the caller may have rewritten its buffer since zfp_compress filled the cache: compare every word
+    if (!dev_stream) {
+      cached = hash_words((const uint64_t*)s->begin, st->words) == st->hash;
+    } else {
+      uint64_t differ = 1;
+      if (gcow::launch_words_differ((const uint64_t*)s->begin, (const uint64_t*)st->d_stream, st->words, st->d_u64 + 2,
+                                    nullptr) != hipSuccess ||
+          hipMemcpy(&differ, st->d_u64 + 2, 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return 0;
+      cached = differ == 0;
+    }
   }
-  if (!st->d_u64 && hipMalloc((void**)&st->d_u64, 16) != hipSuccess) return 0;
   const void* d_stream;
   const uint64_t* d_index = nullptr;
   uint32_t stride = 0;

@@ -14,6 +14,8 @@
 //   k_stage_*          per-stage kernels for parity bisection (hw/stages/*.cpp counterparts)
 //   k_fill_normal      deterministic synthetic gradients
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -613,6 +615,31 @@ __global__ __launch_bounds__(T) void k_encode_fixed1d_np(const void* __restrict_
       encode_block<1>(rw, f, p);
       w = WB == 64 ? rw.acc : (rw.acc & ((1ull << WB) - 1ull));
     }
+    pipe_store<WB>((b0 + T * k) * (WB / 8), rout, w);
+  }
+}
+
+// The memory floor of the fixed-rate 1-D encoder's access pattern (bench.py `roofline.copy_ceiling`): the same
+// one-shot grid, U = 8 blocks per lane, the same raw buffer loads (16 B fp32 / 8 B bf16 per block) and WB-bit
+// non-temporal stores with the same hand-counted waits, and no coding (each block's store is an xor-fold of its load).
+template <int DT, uint32_t WB, int U>
+__global__ __launch_bounds__(256) void k_copy_pattern1d(const void* __restrict__ in, uint32_t nfull,
+                                                        void* __restrict__ out)
+{
+  constexpr uint32_t T = 256;
+  constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;
+  const pipe_v4i rin = buf_rsrc(in, nfull * IB), rout = buf_rsrc(out, nfull * (WB / 8));
+  const uint32_t b0 = blockIdx.x * (T * U) + threadIdx.x;
+  typename PipeRow<DT>::T r[U];
+#pragma unroll
+  for (int k = 0; k < U; k++) r[k] = PipeRow<DT>::load((b0 + T * k) * IB, rin);
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    pipe_wait<U - 1>(r[k]);
+    float f[4];
+    PipeRow<DT>::unpack(r[k], f);
+    const uint64_t w = ((uint64_t)(__float_as_uint(f[0]) ^ __float_as_uint(f[1])) << 32) |
+                       (__float_as_uint(f[2]) ^ __float_as_uint(f[3]));
     pipe_store<WB>((b0 + T * k) * (WB / 8), rout, w);
   }
 }
@@ -1860,6 +1887,17 @@ static void scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* base, 
 
 __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 
+// zfp_decompress's cache check: flag = 1 where the caller's device stream differs from the cached copy (plain
+// vector stores of the same value; the flag was zeroed by a preceding launch on the stream)
+__global__ void k_words_differ(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, uint64_t n,
+                               uint64_t* __restrict__ flag)
+{
+  bool d = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    d = d || a[i] != b[i];
+  if (d) *flag = 1ull;
+}
+
 // ------------------------------------------------------------------------------------------------ header stream
 // dst = header bits [0, off) followed by src bits [0, *d_bits), flushed to whole words (zfp_write_header then
 // zfp_compress at the following bit). Plain stores, one lane per destination word; lanes past the end exit. Lane 0
@@ -2062,6 +2100,45 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
   }
 }
 
+// Variable rate outside the closed-form domain (expert parameters with minbits > 1 or maxbits < 160: a budget can
+// truncate blocks): one lane per 16-block index chunk, the generic libzfp decoder (decode_block) on each stream in
+// rank order, the same fp32 accumulation as above.
+__global__ __launch_bounds__(256) void k_decode_mean1d_generic(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                               uint64_t stream_words, const uint64_t* __restrict__ index,
+                                                               uint64_t index_words, uint64_t nchunks,
+                                                               uint32_t nstreams)
+{
+#pragma clang fp contract(off)
+  const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (c >= nchunks) return;
+  const uint64_t b0 = c * 16, b1 = min<uint64_t>(b0 + 16, F.nblocks);
+  float acc[16][4];
+#pragma unroll
+  for (int k = 0; k < 16; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
+  for (uint32_t r = 0; r < nstreams; r++) {
+    BitReader rd{in + (uint64_t)r * stream_words, index[(uint64_t)r * index_words + c]};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (b0 + k < b1) {
+        float f[4];
+        decode_block<1>(rd, p, f);
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[k][i] = acc[k][i] + f[i];
+      }
+    }
+  }
+  const float nf = (float)nstreams;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    if (b0 + k < b1) {
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) v[i] = acc[k][i] / nf;
+      scatter_block<1>(F, (uint32_t)(b0 + k), v);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ stages
 template <int D>
 __global__ void k_stage_emax(const float* __restrict__ blocks, uint32_t n, int32_t* __restrict__ emax)
@@ -2218,6 +2295,27 @@ static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, vo
   if (nvals % 4) k_encode_fixed1d_tail<DT, WB><<<1, 128, 0, st>>>(in, nvals, nfull, p, out);
 }
 
+hipError_t launch_copy_pattern1d(const void* in, int dtype, uint64_t nvals, uint32_t wb, void* out, void* stream)
+{
+  const uint32_t nfull = (uint32_t)(nvals / 4);
+  constexpr uint32_t CH = 1u << 27;
+  const uint32_t IB = dtype == DT_BF16 ? 8u : 16u;
+  for (uint32_t c0 = 0; c0 < nfull; c0 += CH) {
+    const uint32_t nc = std::min(CH, nfull - c0);
+    const void* ic = (const char*)in + (size_t)c0 * IB;
+    void* oc = (char*)out + (size_t)c0 * (wb / 8);
+    const uint32_t g = (nc + 2047) / 2048;
+    if (dtype == DT_BF16) {
+      if (wb == 64) k_copy_pattern1d<DT_BF16, 64, 8><<<g, 256, 0, S(stream)>>>(ic, nc, oc);
+      else k_copy_pattern1d<DT_BF16, 32, 8><<<g, 256, 0, S(stream)>>>(ic, nc, oc);
+    } else {
+      if (wb == 64) k_copy_pattern1d<DT_F32, 64, 8><<<g, 256, 0, S(stream)>>>(ic, nc, oc);
+      else k_copy_pattern1d<DT_F32, 32, 8><<<g, 256, 0, S(stream)>>>(ic, nc, oc);
+    }
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_encode_fixed1d(const void* in, int dtype, uint64_t nvals, uint32_t nblocks, const Params& p,
                                  void* out, void* stream)
 {
@@ -2349,6 +2447,16 @@ hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream)
   return hipGetLastError();
 }
 
+hipError_t launch_words_differ(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* flag, void* stream)
+{
+  k_set_u64<<<1, 1, 0, S(stream)>>>(flag, 0ull);
+  if (n) {
+    const uint64_t g = std::min<uint64_t>((n + 255) / 256, 4096);
+    k_words_differ<<<(uint32_t)g, 256, 0, S(stream)>>>(a, b, n, flag);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_prepend_header(uint64_t* dst, uint32_t off, const uint64_t* src, const uint64_t* d_bits,
                                  const uint64_t* header, uint64_t max_words, uint64_t* d_total, void* stream)
 {
@@ -2390,6 +2498,11 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
     return hipGetLastError();
   }
   const uint64_t nchunks = (F.nblocks + 15) / 16;
+  if (!(p.minbits <= 1 && p.maxbits >= 160)) {  // a budget can truncate blocks: generic decoder
+    k_decode_mean1d_generic<<<(uint32_t)((nchunks + 255) / 256), 256, 0, st>>>(F, p, in, stream_words, index,
+                                                                              index_words, nchunks, nstreams);
+    return hipGetLastError();
+  }
   k_decode_mean1d_var<128><<<(uint32_t)((nchunks + 127) / 128), 128, 0, st>>>(F, p, in, stream_words, index,
                                                                                index_words, nchunks, nstreams);
   return hipGetLastError();

@@ -67,6 +67,9 @@ hipError_t launch_encode_tiles23(const FieldDesc& F, const Params& p, const Tile
 hipError_t launch_scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* base, uint64_t* total, uint32_t* out32,
                               const uint64_t* d_base, void* stream);
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
+hipError_t launch_copy_pattern1d(const void* in, int dtype, uint64_t nvals, uint32_t wb, void* out, void* stream);
+// *flag = 0, then 1 if a[i] != b[i] for any i < n
+hipError_t launch_words_differ(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* flag, void* stream);
 hipError_t launch_prepend_header(uint64_t* dst, uint32_t off, const uint64_t* src, const uint64_t* d_bits,
                                  const uint64_t* header, uint64_t max_words, uint64_t* d_total, void* stream);
 hipError_t launch_stitch(uint64_t* dst, uint64_t off, const uint64_t* src, uint64_t bits, void* stream);

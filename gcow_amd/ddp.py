@@ -15,6 +15,9 @@ PCIe copies per step. Two device-resident replacements:
 Both register with `ddp_model.register_comm_hook(GcowHookState(...), hook)`. `GcowHookState.codec` defaults to the
 device codec (gcow_amd.dist.DeviceCodec); tests inject an oracle-backed codec to run the hook bodies over gloo.
 """
+import contextlib
+import queue
+import threading
 from dataclasses import dataclass, field
 
 import torch
@@ -32,9 +35,21 @@ class GcowHookState:
     params: GcowParams = field(default_factory=lambda: _codec.rate(16, 1))
     process_group: object = None
     codec: object = None  # None: gcow_amd.dist.device_codec()
+    _worker: object = field(default=None, repr=False)
+    _side: dict = field(default_factory=dict, repr=False)
 
     def get_codec(self):
         return self.codec or gdist.device_codec()
+
+    def worker(self) -> "_CommWorker":
+        if self._worker is None:
+            self._worker = _CommWorker()
+        return self._worker
+
+    def side_stream(self, dev):
+        if dev not in self._side:
+            self._side[dev] = torch.cuda.Stream(dev)
+        return self._side[dev]
 
 
 def _done(t: torch.Tensor) -> torch.futures.Future[torch.Tensor]:
@@ -68,8 +83,38 @@ def roundtrip_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.T
     return fut.then(lossy)
 
 
+class _CommWorker:
+    """One FIFO thread per hook state for the variable-rate exchange: its host read of the gathered lengths (which
+    size the padded all-gather) blocks this thread only, never the autograd thread, and the collectives it issues
+    keep DDP's bucket order on every rank (one queue)."""
+
+    def __init__(self):
+        self.q = queue.Queue()
+        self.t = threading.Thread(target=self._loop, name="gcow-comm", daemon=True)
+        self.t.start()
+
+    def _loop(self):
+        while True:
+            fn, fut = self.q.get()
+            try:
+                fut.set_result(fn())
+            except Exception as ex:  # surfaces in DDP's wait on the hook future
+                fut.set_exception(ex)
+
+    def submit(self, fn, fut):
+        self.q.put((fn, fut))
+        return fut
+
+
 def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.Tensor]:
-    """Encode locally, all-gather the compressed streams, decode every rank's stream and average (one launch)."""
+    """Encode locally, all-gather the compressed streams, decode every rank's stream and average (one launch).
+
+    Asynchronous: the hook enqueues and returns, so bucket i's exchange overlaps the backward of the next buckets
+    (DDP's point; hw/models/train_imagenet.py:194-195, 219, 224 relies on it). Fixed rate chains encode -> all-gather
+    (async_op) -> decode-mean through Future.then. Variable rate needs the gathered lengths on the host to size the
+    padded all-gather; that read and the collectives after it run on the state's comm thread (on a side stream that
+    waits for the encode), and the returned future completes when the mean is written. Each bucket encodes into its
+    own buffers (slot = bucket index), so a later bucket's encode never overwrites a stream still in flight."""
     group = state.process_group
     buf = bucket.buffer()
     world = dist.get_world_size(group)
@@ -77,20 +122,45 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
     n = x.numel()
     p = state.params
     cdc = state.get_codec()
+    slot = bucket.index() if hasattr(bucket, "index") else None
     if _codec.is_fixed(p):
-        words, _, _ = cdc.encode(x, p)
+        words, _, _ = cdc.encode(x, p, 0, slot=slot)
         nw = ((n + 3) // 4 * p.maxbits + 63) // 64
-        gathered = gdist.allgather_padded(words, nw, nw, group, pad=2)
-        mean = cdc.decode_mean(gathered, nw, world, n, p)
+        gathered = torch.zeros(world * nw + 2, dtype=torch.int64, device=x.device)
+        fut = gdist.allgather_into_async(gathered[: world * nw], words[:nw].contiguous(), group)
+
+        def finish(f):
+            f.wait()
+            mean = cdc.decode_mean(gathered, nw, world, n, p)
+            flat.copy_(mean.to(flat.dtype))
+            return buf
+
+        return fut.then(finish)
+    words, bits, index = cdc.encode(x, p, INDEX_STRIDE, slot=slot)
+    dev = x.device
+    if dev.type == "cuda":
+        ev = torch.cuda.Event()
+        ev.record()
+        side = state.side_stream(dev)
+        fut = torch.futures.Future(devices=[dev])
     else:
-        words, bits, index = cdc.encode(x, p, INDEX_STRIDE)
-        lens, lens_h = gdist.gather_lengths(bits, x.device, group)
-        maxw = max(1, max((b + 63) // 64 for b in lens_h))
-        rank = dist.get_rank(group)
-        gathered = gdist.allgather_padded(words, (lens_h[rank] + 63) // 64, maxw, group, pad=2)
-        ni = index.numel()
-        idx = torch.empty(world * ni, dtype=torch.int64, device=x.device)
-        gdist.allgather_into(idx, index[:ni].contiguous(), group)
-        mean = cdc.decode_mean(gathered, maxw, world, n, p, idx, ni, INDEX_STRIDE)
-    flat.copy_(mean.to(flat.dtype))
-    return _done(buf)
+        ev = side = None
+        fut = torch.futures.Future()
+
+    def exchange():
+        ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
+        with ctx:
+            if side is not None:
+                side.wait_event(ev)
+            lens, lens_h = gdist.gather_lengths(bits, dev, group)  # host read: this thread waits, autograd does not
+            maxw = max(1, max((b + 63) // 64 for b in lens_h))
+            rank = dist.get_rank(group)
+            gathered = gdist.allgather_padded(words, (lens_h[rank] + 63) // 64, maxw, group, pad=2)
+            ni = index.numel()
+            idx = torch.empty(world * ni, dtype=torch.int64, device=dev)
+            gdist.allgather_into(idx, index[:ni].contiguous(), group)
+            mean = cdc.decode_mean(gathered, maxw, world, n, p, idx, ni, INDEX_STRIDE)
+            flat.copy_(mean.to(flat.dtype))
+            return buf  # set_result inside the side-stream context: waiters sync on this stream's work
+
+    return state.worker().submit(exchange, fut)

@@ -30,11 +30,13 @@ class DeviceCodec:
     def __init__(self):
         self._enc = {}
 
-    def encode(self, x: torch.Tensor, params, index_stride: int = 0):
-        """-> (words int64 tensor, bits int64[1] tensor on x.device, block index or None)."""
+    def encode(self, x: torch.Tensor, params, index_stride: int = 0, slot=None):
+        """-> (words int64 tensor, bits int64[1] tensor on x.device, block index or None). Calls with the same shape,
+        params and `slot` reuse (overwrite) one set of output buffers; callers whose streams are still in flight on
+        another stream pass distinct slots (the DDP hook: one per bucket)."""
         from . import codec
         x = x.reshape(-1)
-        key = (x.numel(), x.dtype, x.device, params.tuple(), index_stride)
+        key = (slot, x.numel(), x.dtype, x.device, params.tuple(), index_stride)
         enc = self._enc.get(key)
         if enc is None:
             enc = self._enc[key] = codec.Encoder((x.numel(),), x.dtype, params, x.device, index_stride)
@@ -90,6 +92,17 @@ def allgather_into(out: torch.Tensor, local: torch.Tensor, group=None):
         world = dist.get_world_size(group)
         dist.all_gather(list(out.chunk(world)), local, group=group)
     return out
+
+
+def allgather_into_async(out: torch.Tensor, local: torch.Tensor, group=None) -> torch.futures.Future:
+    """allgather_into with async_op=True: -> the collective's Future (RCCL: completed once enqueued, its waiters
+    synchronise on the collective's stream; gloo: completed when the data has arrived)."""
+    if is_nccl(group):
+        work = dist.all_gather_into_tensor(out, local, group=group, async_op=True)
+    else:
+        world = dist.get_world_size(group)
+        work = dist.all_gather(list(out.chunk(world)), local, group=group, async_op=True)
+    return work.get_future()
 
 
 def allgather_fixed(words: torch.Tensor, nblocks: int, maxbits: int, group=None) -> torch.Tensor:

@@ -266,13 +266,16 @@ gcow_status gcow_stitch_shards_device(uint64_t* d_dst, uint64_t dst_words, const
  * Decode-and-average of nstreams 1-D streams of one bucket shape (the compressed all-gather DDP hook's receive side;
  * hw/models/train_imagenet.py:446-475 is the caller contract): field->data (DEVICE fp32, 1-D) receives, elementwise
  * in fp32, ((0 + x_0) + x_1 + ... + x_{n-1}) / nstreams with x_r the libzfp decode of stream r. Streams start
- * stream_words words apart at d_streams; the buffer must have 2 readable words past the last stream. Fixed rate: any
- * parameters. Variable rate: minbits <= 1, maxbits >= 160 (accuracy / precision / expert) and every stream's block
- * index (index_stride 16, entries index_words apart at d_index, as gcow_encode_device writes them).
+ * stream_words words apart at d_streams; streams_bytes is the buffer's size, which must cover nstreams * stream_words
+ * + 2 words (the decoders read 64-bit windows past a stream's last bit; GCOW_ERR_INVALID otherwise). Fixed rate: any
+ * parameters, d_index NULL and index_words = index_stride = 0. Variable rate: any parameters (minbits <= 1,
+ * maxbits >= 160 take the closed-form decoder, others the generic one) and every stream's block index (index_stride
+ * 16, entries index_words apart at d_index, as gcow_encode_device writes them).
  */
 gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p, const uint64_t* d_streams,
-                                    uint64_t stream_words, uint32_t nstreams, const uint64_t* d_index,
-                                    uint64_t index_words, uint32_t index_stride, void* hip_stream);
+                                    size_t streams_bytes, uint64_t stream_words, uint32_t nstreams,
+                                    const uint64_t* d_index, uint64_t index_words, uint32_t index_stride,
+                                    void* hip_stream);
 
 /*
  * zfp 0.5.5 stream header: the byte format zfpy.compress_numpy writes (hw/models/train_imagenet.py:459-465 calls
@@ -313,6 +316,12 @@ gcow_status gcow_stage_reorder_device(const int32_t* d_iblocks, uint32_t nblocks
 gcow_status gcow_stage_encode_ints_device(const uint32_t* d_ublocks, uint32_t nblocks, uint32_t dims,
                                           uint32_t budget, uint32_t maxprec, uint64_t* d_slots, uint32_t slot_words,
                                           uint32_t* d_bits, void* hip_stream);
+
+/* Measurement kernel (bench.py roofline.copy_ceiling): the fixed-rate 1-D encoder's memory access pattern without the
+ * coding -- the same grid, loads of every full 4-value block (16 B fp32 / 8 B bf16) and one out_bits_per_block (32 or
+ * 64) store per block -- i.e. the HBM floor that kernel can reach. Output bytes are not a stream. */
+gcow_status gcow_copy_pattern_device(const void* d_in, int dtype, size_t nvals, uint32_t out_bits_per_block,
+                                     void* d_out, void* hip_stream);
 
 /* Deterministic synthetic gradient bucket on the device (bench / smoke inputs; SURVEY 8(d) distribution):
  * N(0, sigma) via counter-based splitmix64 + Box-Muller, with zero / tiny / subnormal 4-value blocks injected at

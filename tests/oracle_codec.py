@@ -32,7 +32,7 @@ class OracleCodec:
     def __init__(self):
         self.records = []
 
-    def encode(self, x: torch.Tensor, params, index_stride: int = 0):
+    def encode(self, x: torch.Tensor, params, index_stride: int = 0, slot=None):
         a = _np_values(x)
         p = _params(params)
         w, bits = O.compress(a, p)

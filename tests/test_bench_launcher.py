@@ -39,3 +39,18 @@ def test_bench_self_launches_n_ranks(n):
 def test_bench_single_rank():
     d = _run("--gpus", "1")
     assert d["n_gpus"] == 1 and d["ranks"] == [[0, 0, 1, "torchrun"]]
+
+
+def test_bench_programmatic_argv_reaches_ranks():
+    """main(argv) launches its ranks with `argv`, not with the parent's sys.argv."""
+    code = ("import sys; sys.argv = ['bench.py', '--steps', '999']; import bench; "
+            "bench.main(['--stub', '--gpus', '2', '--steps', '2', '--warmup', '1', '--values', '4096'])")
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2

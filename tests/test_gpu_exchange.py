@@ -86,13 +86,24 @@ def _oracle_mean(orc, streams, op, n):
     return acc / np.float32(len(streams))
 
 
-@pytest.mark.parametrize("mode", ["rate16", "rate8", "rate2.5", "expert_generic", "acc1e-6", "acc1e-3", "bf16_acc1e-6"])
+MEAN_MODES = {"rate16": (16,), "rate8": (8,), "rate2.5": (2.5,), "expert_generic": (64, 64, 20, -1074),
+              "acc1e-6": 1e-6, "acc1e-3": 1e-3, "bf16_acc1e-6": 1e-6,
+              # variable rate outside the closed-form domain: minbits > 1 pads, maxbits < 160 truncates
+              "expert_var_minbits": (8, 512, 32, -1074), "expert_var_trunc": (1, 100, 64, -30)}
+
+
+def _mean_op(orc, mode):
+    v = MEAN_MODES[mode]
+    if isinstance(v, float):
+        return orc.accuracy(v)
+    return orc.rate(v[0], 1) if len(v) == 1 else orc.expert(*v)
+
+
+@pytest.mark.parametrize("mode", list(MEAN_MODES))
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_decode_mean_vs_oracle(gc, orc, mode, world):
     n = 4 * 20001 + 2  # a partial last block; > 128 index chunks
-    op = {"rate16": orc.rate(16, 1), "rate8": orc.rate(8, 1), "rate2.5": orc.rate(2.5, 1),
-          "expert_generic": orc.expert(64, 64, 20, -1074), "acc1e-6": orc.accuracy(1e-6),
-          "acc1e-3": orc.accuracy(1e-3), "bf16_acc1e-6": orc.accuracy(1e-6)}[mode]
+    op = _mean_op(orc, mode)
     fixed = op.minbits == op.maxbits
     buckets = [_bucket(orc, n, 900 + r, mode.startswith("bf16")) for r in range(world)]
     encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else 16) for b in buckets]
@@ -111,6 +122,25 @@ def test_decode_mean_vs_oracle(gc, orc, mode, world):
     assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
 
 
+def test_decode_mean_argument_checks(gc, orc):
+    """The C entry validates what its kernels assume: 2 readable words past the last stream, and no block index on
+    the fixed-rate path."""
+    n = 4 * 1000
+    p = gc.rate(16, 1)
+    e = gc.encode(_dev(_bucket(orc, n, 3)), p)
+    sw = e.nwords
+    with pytest.raises(gc.GcowError):
+        gc.decode_mean(e.words[:sw].contiguous(), sw, 1, n, p)  # no padding words
+    buf = torch.zeros(sw + 2, dtype=torch.int64, device="cuda")
+    buf[:sw] = e.stream()
+    with pytest.raises(gc.GcowError):
+        gc.decode_mean(buf, sw, 1, n, p, buf, 1, 16)  # an index on a fixed-rate stream
+    got = gc.decode_mean(buf, sw, 1, n, p)
+    torch.cuda.synchronize()
+    ref = orc.decompress(orc.compress(_bucket(orc, n, 3), orc.rate(16, 1))[0], (n,), orc.rate(16, 1))
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
 # ---------------------------------------------------------------------------------------------- multi-process
 class HostStagedDeviceCodec:
     """gcow_amd.dist.DeviceCodec behind host copies: the exchange code moves CPU tensors over gloo (two processes
@@ -121,8 +151,8 @@ class HostStagedDeviceCodec:
         self.d = DeviceCodec()
         self.calls = []
 
-    def encode(self, x, params, index_stride=0):
-        w, b, i = self.d.encode(x.cuda(), params, index_stride)
+    def encode(self, x, params, index_stride=0, slot=None):
+        w, b, i = self.d.encode(x.cuda(), params, index_stride, slot=slot)
         self.calls.append("encode")
         return w.cpu(), b.cpu(), (i.cpu() if i is not None else None)
 
@@ -236,27 +266,42 @@ def nccl_world1():
 
 
 @pytest.mark.parametrize("hook", ["roundtrip_hook", "compressed_allgather_hook"])
-@pytest.mark.parametrize("mode", ["rate16", "acc1e-6", "rate8"])
+@pytest.mark.parametrize("mode", ["rate16", "acc1e-6", "rate8", "expert_var_minbits", "expert_var_trunc"])
 def test_ddp_hooks_world1_bit_exact(gc, orc, nccl_world1, hook, mode):
-    """One rank over RCCL: the weight gradient (the whole bucket) equals the oracle's decode(encode(local grad)) --
-    (0 + x) / 1 for the all-gather hook -- bit for bit."""
+    """One rank over RCCL: every weight gradient equals the oracle's decode(encode(local grad)) -- (0 + x) / 1 for the
+    all-gather hook -- bit for bit. Three equal-size layers give three buckets of one shape in
+    flight at once (the asynchronous hook must not let a later bucket's encode overwrite an earlier stream), and two
+    training steps reuse every buffer."""
     from gcow_amd import ddp
-    params = {"rate16": gc.rate(16, 1), "acc1e-6": gc.accuracy(1e-6), "rate8": gc.rate(8, 1)}[mode]
+    params = {"rate16": gc.rate(16, 1), "acc1e-6": gc.accuracy(1e-6), "rate8": gc.rate(8, 1),
+              "expert_var_minbits": gc.expert(8, 512, 32, -1074), "expert_var_trunc": gc.expert(1, 100, 64, -30)}[mode]
     torch.manual_seed(0)
-    model = torch.nn.Linear(64, 97, bias=False).cuda()
-    ref = torch.nn.Linear(64, 97, bias=False).cuda()
+    # 640 x 640 fp32 weights (1.6 MB) each fill a bucket of their own past DDP's 1 MiB first-bucket cap
+    layers = lambda: torch.nn.Sequential(*[torch.nn.Linear(640, 640, bias=False) for _ in range(3)]).cuda()  # noqa
+    model, ref = layers(), layers()
     ref.load_state_dict(model.state_dict())
-    dm = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0])
-    dm.register_comm_hook(ddp.GcowHookState(params=params), getattr(ddp, hook))
-    x = torch.randn(32, 64, device="cuda")
-    dm(x).square().mean().backward()
-    ref(x).square().mean().backward()
-    g = ref.weight.grad.reshape(-1).cpu().numpy()
+    dm = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=1)
+    seen = []
+
+    def counted(state, bucket):
+        seen.append(bucket.index())
+        return getattr(ddp, hook)(state, bucket)
+
+    dm.register_comm_hook(ddp.GcowHookState(params=params), counted)
     op = orc.expert(*params.tuple())
-    dec = orc.decompress(orc.compress(g, op)[0], g.shape, op)
-    want = (np.zeros_like(dec) + dec) / np.float32(1) if hook == "compressed_allgather_hook" else dec
-    got = model.weight.grad.reshape(-1).cpu().numpy()
-    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    for step in range(2):
+        model.zero_grad()
+        ref.zero_grad()
+        x = torch.randn(32, 640, device="cuda")
+        dm(x).square().mean().backward()
+        ref(x).square().mean().backward()
+        for lm, lr in zip(model, ref):
+            g = lr.weight.grad.reshape(-1).cpu().numpy()
+            dec = orc.decompress(orc.compress(g, op)[0], g.shape, op)
+            want = (np.zeros_like(dec) + dec) / np.float32(1) if hook == "compressed_allgather_hook" else dec
+            got = lm.weight.grad.reshape(-1).cpu().numpy()
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), step
+    assert len(set(seen)) >= 2, seen  # several buckets per step
 
 
 # ---------------------------------------------------------------------------------------------- bench N > 1 legs

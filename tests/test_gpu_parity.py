@@ -431,6 +431,57 @@ def test_dropin_decompress_sees_rewritten_stream(gc, orc):
     L.cleanup(inp, out)
 
 
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_dropin_decompress_sees_one_word_edit(gc, orc, where):
+    """A local edit of ONE word of the stream (any word, not a sampled one) between zfp_compress and zfp_decompress is
+    decoded: the cache check covers every word (host: a hash of all words; device: a device-side compare)."""
+    from gcow_amd import _ffi
+    L = _ffi.load()
+    n = 4 * 5000
+    a = orc.gen_normal(n, 1e-3, 5, True)
+    op = orc.rate(16, 1)
+    w, _ = orc.compress(a, op)
+    inp = _host_input(L, a, 1)
+    out = L.init_zfp_output(inp)
+    assert L.set_zfp_output_expert(out, *op.tuple()) == 1
+    dbuf = None
+    if where == "device":
+        dbuf = torch.zeros(w.size + 8, dtype=torch.int64, device="cuda")
+        out.contents.data = L.stream_init(C.c_void_p(dbuf.data_ptr()), dbuf.numel() * 8)
+    assert L.zfp_compress(out, inp) == w.nbytes
+    k = 3001  # word 3001 = block 3001 at rate 16
+    edited = w.copy()
+    edited[k] ^= np.uint64(0x5A5A5A5A00000000)
+    if where == "device":
+        torch.cuda.synchronize()
+        dbuf[k] = int(edited.view(np.int64)[k])
+        torch.cuda.synchronize()
+    else:
+        C.memmove(out.contents.data.contents.begin, edited.ctypes.data, edited.nbytes)
+    L.stream_rewind(out.contents.data)
+    back = np.zeros_like(a)
+    inp2 = L.alloc_zfp_input()
+    inp2.contents.dtype = 3
+    inp2.contents.data = back.ctypes.data
+    inp2.contents.nx = n
+    L.zfp_decompress(out, inp2)
+    want = orc.decompress(edited, a.shape, op)
+    assert not np.array_equal(want.view(np.uint32), orc.decompress(w, a.shape, op).view(np.uint32))
+    assert np.array_equal(back.view(np.uint32), want.view(np.uint32))
+    # unedited: the cached device copy is used and decodes the same
+    if where == "device":
+        dbuf[k] = int(w.view(np.int64)[k])
+        torch.cuda.synchronize()
+    else:
+        C.memmove(out.contents.data.contents.begin, w.ctypes.data, w.nbytes)
+    L.stream_rewind(out.contents.data)
+    L.zfp_decompress(out, inp2)
+    assert np.array_equal(back.view(np.uint32), orc.decompress(w, a.shape, op).view(np.uint32))
+    inp2.contents.data = None
+    L.free_zfp_input(inp2)
+    L.cleanup(inp, out)  # a device stream's buffer is the caller's (not freed)
+
+
 def test_block_api_known_answers(gc, orc):
     """sw/tests/test_stages.cpp ENCODE_IBLOCK / ENCODE_ALL_BITPLANES / CAST through the drop-in block API."""
     from gcow_amd import _ffi
@@ -499,10 +550,15 @@ def test_encode_fblock_decode_fblock(gc, orc):
 
 # ---------------------------------------------------------------------------------------------- full-size configs
 def test_c2_full_size_fixed_rate(gc, orc):
-    """BASELINE config 2: 256 Mi contiguous fp32, 1-D fixed rate 16 and 8, bit-exact vs the threaded oracle."""
+    """BASELINE config 2: 256 Mi contiguous fp32, 1-D fixed rate 16 and 8, bit-exact vs the threaded oracle -- on the
+    very bucket bench.py times (codec.fill_normal, seed 0x67636F77, zero / tiny / subnormal blocks injected)."""
     n = 256 * 1024 * 1024
-    a = orc.gen_normal(n, 1e-3, 0x67636F77, True)
-    x = torch.from_numpy(a).cuda()
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    gc.fill_normal(x, 1e-3, seed=0x67636F77, inject=True)
+    a = x.cpu().numpy()
+    # the injected special blocks are there (bench.data claims them)
+    blk = np.abs(a.reshape(-1, 4)).max(axis=1)
+    assert (blk == 0).sum() > n // 4 // 128 and ((blk > 0) & (blk < 2.0 ** -98)).sum() > n // 4 // 4096
     for r in (16, 8):
         op = orc.rate(r, 1)
         w_ref, bits_ref = orc.compress(a, op, threads=min(16, os.cpu_count() or 1))
@@ -523,16 +579,10 @@ def test_c2_full_size_fixed_rate(gc, orc):
 
 
 def test_c3_full_size_roundtrip(gc, orc):
-    """BASELINE config 3: 512^3 fp32 volume, 3-D fixed rate 8 and accuracy 1e-3, encode + decode vs the oracle."""
-    n = 512
-    x = np.arange(n, dtype=np.float64) / n
-    g = (np.sin(6 * np.pi * x)[None, None, :].astype(np.float32) *
-         np.cos(4 * np.pi * x)[None, :, None].astype(np.float32) *
-         np.sin(2 * np.pi * x)[:, None, None].astype(np.float32))
-    g += 1e-3 * orc.gen_normal(n ** 3, 1.0, 21, False).reshape(n, n, n)
-    a = np.ascontiguousarray(g, dtype=np.float32)
-    del g
-    xt = torch.from_numpy(a).cuda()
+    """BASELINE config 3: 512^3 fp32 volume, 3-D fixed rate 8 and accuracy 1e-3, encode + decode vs the oracle -- on
+    the field bench.py times (codec.c3_field)."""
+    xt = gc.c3_field(torch.device("cuda", 0))
+    a = xt.cpu().numpy()
     for op, stride in ((orc.rate(8, 3), 0), (orc.accuracy(1e-3), 1)):
         w_ref, bits_ref = orc.compress(a, op, threads=min(16, os.cpu_count() or 1))
         e = gc.encode(xt, P(gc, op), index_stride=stride)
@@ -548,6 +598,40 @@ def test_c3_full_size_roundtrip(gc, orc):
         if op.minbits != op.maxbits:
             assert float(np.max(np.abs(d - a))) <= 1e-3
         del w_ref, d
+
+
+def test_multichunk_fixed_rate_1d(gc, orc):
+    """More than 2^27 blocks: the fixed-rate 1-D encoder and decoder launch the grid in chunks of 2^27 blocks (buffer
+    offsets stay below 2^32; gcow_kernels.hip launch_fixed1d_t / launch_decode_fixed1d), as C4's strong-scaling legs
+    do with 1-2 Gi values per rank. n = 2^29 + 4 * 1001 + 3 values (2 GiB): two chunks and a padded last block. Whole
+    stream vs the threaded oracle at rates 16 and 8; the decode vs the oracle on windows across the chunk boundary,
+    a random interior window and the tail."""
+    n = (1 << 29) + 4 * 1001 + 3
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    gc.fill_normal(x, 1e-3, seed=0x67636F77 + 99, inject=True)
+    a = x.cpu().numpy()
+    nb = (n + 3) // 4
+    ch = 1 << 27
+    rng = np.random.default_rng(29)
+    mid = int(rng.integers(1, ch // 16)) * 16
+    windows = [(ch - 4096, ch + 4096), (mid, mid + 8192), (nb - 1001 - 16 * 40, nb)]
+    for r in (16, 8):
+        op = orc.rate(r, 1)
+        w_ref, bits_ref = orc.compress(a, op, threads=min(16, os.cpu_count() or 1))
+        e = gc.encode(x, P(gc, op))
+        torch.cuda.synchronize()
+        assert e.bits == bits_ref == nb * 4 * r
+        got = e.stream().cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, w_ref)
+        del got
+        d = gc.decode(e)
+        torch.cuda.synchronize()
+        for b0, b1 in windows:  # b0 % 16 == 0: the window starts on a stream word at both rates
+            lo, hi = 4 * b0, min(4 * b1, n)
+            ws = w_ref[b0 * 4 * r // 64:(b1 * 4 * r + 63) // 64]
+            ref = orc.decompress(ws, (hi - lo,), op)
+            assert np.array_equal(d[lo:hi].cpu().numpy().view(np.uint32), ref.view(np.uint32)), (r, b0, b1)
+        del d, e, w_ref
 
 
 @pytest.mark.parametrize("r", [16, 8])
