@@ -67,6 +67,11 @@ hipError_t launch_encode_tiles23(const FieldDesc& F, const Params& p, const Tile
 hipError_t launch_scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* base, uint64_t* total, uint32_t* out32,
                               const uint64_t* d_base, void* stream);
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
+// Single-pass 1-D variable-rate encoder (var1d.hip): minbits <= 1, maxbits >= 160; ws = var1d_sp_workspace_bytes().
+size_t var1d_sp_workspace_bytes(uint64_t nblocks);
+hipError_t launch_encode1d_var_sp(const FieldDesc& F, const Params& p, uint32_t* out32, uint64_t* ws,
+                                  uint64_t* d_total, uint64_t* index, uint32_t index_shift, const uint64_t* d_base,
+                                  void* stream);
 hipError_t launch_copy_pattern1d(const void* in, int dtype, uint64_t nvals, uint32_t wb, void* out, void* stream);
 // *flag = 0, then 1 if a[i] != b[i] for any i < n
 hipError_t launch_words_differ(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* flag, void* stream);

@@ -75,7 +75,9 @@ def roundtrip_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.T
         t = f.value()[0]
         flat, x = _flat(t)
         stride = 0 if _codec.is_fixed(state.params) else INDEX_STRIDE
-        words, _, index = cdc.encode(x, state.params, stride)
+        # per-bucket buffers: DDP may run several buckets' callbacks before the first one's decode has read its words
+        words, _, index = cdc.encode(x, state.params, stride,
+                                     slot=("roundtrip", bucket.index() if hasattr(bucket, "index") else None))
         out = cdc.decode(words, x.numel(), state.params, index=index, index_stride=stride)
         flat.copy_(out.to(flat.dtype))
         return t
@@ -97,9 +99,10 @@ class _CommWorker:
         while True:
             fn, fut = self.q.get()
             try:
-                fut.set_result(fn())
+                fn(fut)  # completes fut itself, inside its stream context
             except Exception as ex:  # surfaces in DDP's wait on the hook future
-                fut.set_exception(ex)
+                if not fut.done():
+                    fut.set_exception(ex)
 
     def submit(self, fn, fut):
         self.q.put((fn, fut))
@@ -147,7 +150,7 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
         ev = side = None
         fut = torch.futures.Future()
 
-    def exchange():
+    def exchange(fut):
         ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
         with ctx:
             if side is not None:
@@ -161,6 +164,8 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
             gdist.allgather_into(idx, index[:ni].contiguous(), group)
             mean = cdc.decode_mean(gathered, maxw, world, n, p, idx, ni, INDEX_STRIDE)
             flat.copy_(mean.to(flat.dtype))
-            return buf  # set_result inside the side-stream context: waiters sync on this stream's work
+            # completed inside the side-stream context: the future records its event on this stream, so DDP's wait
+            # orders its use of the bucket after the mean is written
+            fut.set_result(buf)
 
     return state.worker().submit(exchange, fut)

@@ -703,6 +703,27 @@ def test_var1d_closed_form_coder(gc, orc, mode):
     _check_vs_oracle(gc, orc, a, op, index_stride=16)
 
 
+@pytest.mark.parametrize("env", ["spin0", "two_pass"])
+@pytest.mark.parametrize("mode", ["acc1e-6", "acc1e-3", "prec32", "expert_max", "bf16_acc1e-6"])
+def test_var1d_encoder_forms(gc, orc, env, mode, monkeypatch):
+    """The 1-D variable-rate encoder's other forms, bit-exact vs the oracle: `spin0` makes every tile of the
+    single-pass encoder compute a not-yet-published predecessor's total itself (its no-dispatch-order fallback; the
+    default waits for the predecessor first), `two_pass` is the count + scan + encode form (GCOW_VAR1D_TWO_PASS)."""
+    monkeypatch.setenv({"spin0": "GCOW_VAR1D_SPIN", "two_pass": "GCOW_VAR1D_TWO_PASS"}[env], "0" if env == "spin0" else "1")
+    a = np.concatenate([_adversarial_1d(11), orc.gen_normal((1 << 20) + 3, 1e-3, 78, True)])
+    if mode.startswith("bf16"):
+        a = (a.view(np.uint32) >> 16).astype(np.uint16)
+    op = {"acc1e-6": orc.accuracy(1e-6), "acc1e-3": orc.accuracy(1e-3), "prec32": orc.precision(32),
+          "expert_max": orc.expert(1, 16658, 64, -1074), "bf16_acc1e-6": orc.accuracy(1e-6)}[mode]
+    w_ref, bits_ref = orc.compress(a, op)
+    e, b = dev_encode_bytes(gc, a, P(gc, op), 16)
+    assert e.bits == bits_ref
+    assert b == w_ref.tobytes()
+    d = gc.decode(e)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy().view(np.uint32), orc.decompress(w_ref, a.shape, op).view(np.uint32))
+
+
 def test_c5_full_size_bf16_accuracy(gc, orc):
     """BASELINE config 5 shape: 256 Mi bf16 values (exact widening), accuracy 1e-6, vs the threaded oracle."""
     n = 256 * 1024 * 1024
