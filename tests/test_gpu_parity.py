@@ -614,7 +614,7 @@ def test_multichunk_fixed_rate_1d(gc, orc):
     ch = 1 << 27
     rng = np.random.default_rng(29)
     mid = int(rng.integers(1, ch // 16)) * 16
-    windows = [(ch - 4096, ch + 4096), (mid, mid + 8192), (nb - 1001 - 16 * 40, nb)]
+    windows = [(ch - 4096, ch + 4096), (mid, mid + 8192), ((nb - 1001 - 16 * 40) // 16 * 16, nb)]
     for r in (16, 8):
         op = orc.rate(r, 1)
         w_ref, bits_ref = orc.compress(a, op, threads=min(16, os.cpu_count() or 1))

@@ -71,14 +71,7 @@ def c2_decode():
 
 
 def c3():
-    n = 512
-    g = torch.arange(n, device="cuda", dtype=torch.float64) / n
-    x = (torch.sin(6 * math.pi * g)[None, None, :] * torch.cos(4 * math.pi * g)[None, :, None] *
-         torch.sin(2 * math.pi * g)[:, None, None]).float()
-    noise = torch.empty(n ** 3, dtype=torch.float32, device="cuda")
-    codec.fill_normal(noise, 1e-3, inject=False)
-    x += noise.view(n, n, n)
-    del noise
+    x = codec.c3_field("cuda")  # the field bench.py times and tests/test_gpu_parity.py checks
     for name, p, stride in (("rate8", codec.rate(8, 3), 0), ("acc1e-3", codec.accuracy(1e-3), 1)):
         enc = codec.Encoder(x.shape, torch.float32, p, index_stride=stride)
         ms_e = timeit(lambda: enc(x), reps=5)

@@ -44,6 +44,17 @@ def c3(reps):
         torch.cuda.synchronize()
 
 
+def c3dec(reps):
+    """The C3 rate-8 and accuracy-1e-3 decoders alone (streams encoded once, untimed), on the bench's C3 field."""
+    x = codec.c3_field("cuda")
+    for p, stride in ((codec.rate(8, 3), 0), (codec.accuracy(1e-3), 1)):
+        e = codec.Encoder(x.shape, torch.float32, p, index_stride=stride)(x)
+        out = torch.empty_like(x)
+        for _ in range(reps):
+            codec.decode(e, out=out)
+        torch.cuda.synchronize()
+
+
 def c5(reps):
     n = 256 << 20
     xf = torch.empty(n, dtype=torch.float32, device="cuda")
