@@ -247,7 +247,7 @@ __device__ __forceinline__ void v1_prepare(const FieldDesc& F, const Params& p, 
     lsum += T.len[k];
   }
   T.excl = block_exclusive_scan<V1T>(lsum, &T.total, scan_sh);
-  if (threadIdx.x == 0)  // incl_base given (tile 0): the inclusive prefix at once
+  if (status && threadIdx.x == 0)  // incl_base given (tile 0): the inclusive prefix at once
     __hip_atomic_store(status + t, incl_base != ~0ull ? ((2ull << 62) | (incl_base + T.total)) : ((1ull << 62) | T.total),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -353,13 +353,16 @@ __device__ uint64_t v1_lookback(uint64_t* status, uint32_t t, uint64_t base0, co
 // lanes' offsets by a workgroup scan) and publish its total at once; code into the LDS window at tile-relative
 // positions; look back (one wave) for the stream offset; store the window shifted to the offset, the two words shared
 // with the neighbouring tiles through v1_boundary.
-template <int DT>
+// LB = false: the tile's offset is rbase[t] from a count pass and a scan (no status words; the scan zeroed the words
+// two tiles share, so both contributors atomicOr them into the stream).
+template <int DT, bool LB = true>
 __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, uint64_t* __restrict__ status,
                                                          uint64_t* __restrict__ bnd, uint32_t* __restrict__ out32,
                                                          uint64_t* __restrict__ index, uint32_t index_shift,
                                                          const uint64_t* __restrict__ d_base,
                                                          uint64_t* __restrict__ d_total, uint32_t ntiles,
-                                                         uint32_t spin, uint64_t* __restrict__ stats)
+                                                         uint32_t spin, uint64_t* __restrict__ stats,
+                                                         const uint64_t* __restrict__ rbase = nullptr)
 {
   __shared__ uint32_t tab[1280];  // pair table (lean-5 entries, rows n >= 3 empty)
   __shared__ uint32_t rs[1024];   // window spread tables
@@ -374,11 +377,11 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, 
   for (uint32_t i = tid; i < 1024; i += V1T) rs[i] = rspread_entry(i);
   if (tid == 0) s_special = 0;
   const bool wide_ok = F.vec && (((uintptr_t)F.data) & 15u) == 0;
-  const uint64_t base0 = d_base ? *d_base : 0ull;
+  const uint64_t base0 = LB && d_base ? *d_base : 0ull;
   V1Raw<DT> raw;
   raw.load(F, t, wide_ok);
   V1Tile T;
-  v1_prepare<DT>(F, p, raw, t, T, scan_sh, status, t == 0 ? base0 : ~0ull);
+  v1_prepare<DT>(F, p, raw, t, T, scan_sh, LB ? status : nullptr, t == 0 ? base0 : ~0ull);
   const uint32_t excl = T.excl, total = T.total;
   uint32_t lsum = 0;
 #pragma unroll
@@ -452,7 +455,9 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, 
   }
 
   // ---- the tile's stream offset (wave 0)
-  if (tid < 64) {
+  if (!LB) {
+    if (tid == 0) s_base = rbase[t];
+  } else if (tid < 64) {
     const uint64_t B = t == 0 ? base0
                               : ((V1_ABLATE & 1) ? (uint64_t)t << 16
                                                  : v1_lookback<DT>(status, t, base0, F, p, lane, spin, stats));
@@ -487,7 +492,9 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, 
     uint32_t* dst = out32 + g0 + k;
     const bool first = k == 0 && rb != 0;
     const bool tail = k == nw - 1 && ((rb + total) & 31u) != 0 && !last_tile;
-    if (first) {
+    if (!LB && (first || tail)) {
+      atomicOr(dst, val);  // a word shared with a neighbouring tile (zeroed by the scan) or the appended stream
+    } else if (first) {
       if (t == 0) atomicOr(dst, val);  // bits already in the stream before d_base (append)
       else v1_boundary(bnd, t - 1, 1u, dst, val);
     } else if (tail) {
@@ -532,6 +539,22 @@ hipError_t launch_encode1d_var_sp(const FieldDesc& F, const Params& p, uint32_t*
   else
     k_encode1d_var_sp<DT_F32><<<ntiles, V1T, 0, st>>>(F, p, status, bnd, out32, index, index_shift, d_base, d_total,
                                                       ntiles, spin, stats);
+  return hipGetLastError();
+}
+
+uint32_t var1d_tile_blocks() { return V1TILE; }
+
+hipError_t launch_encode1d_var_placed(const FieldDesc& F, const Params& p, uint32_t* out32, const uint64_t* rbase,
+                                      uint64_t* index, uint32_t index_shift, void* stream)
+{
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t ntiles = (uint32_t)((F.nblocks + V1TILE - 1) / V1TILE);
+  if (F.dtype == DT_BF16)
+    k_encode1d_var_sp<DT_BF16, false><<<ntiles, V1T, 0, st>>>(F, p, nullptr, nullptr, out32, index, index_shift,
+                                                              nullptr, nullptr, ntiles, 0, nullptr, rbase);
+  else
+    k_encode1d_var_sp<DT_F32, false><<<ntiles, V1T, 0, st>>>(F, p, nullptr, nullptr, out32, index, index_shift,
+                                                             nullptr, nullptr, ntiles, 0, nullptr, rbase);
   return hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""C5 (256 Mi bf16 1-D, accuracy 1e-6 / 1e-3) and 1-D fp32 variable-rate encode: the single-pass encoder against
-the count + scan + encode form (GCOW_VAR1D_TWO_PASS=1), interleaved in one process. Per form: the driver protocol
+"""C5 (256 Mi bf16 1-D, accuracy 1e-6 / 1e-3) and 1-D fp32 variable-rate encode: the 1-D variable-rate encoder forms
+(FORMS below), interleaved in one process. Per form: the driver protocol
 (5 untimed + 20 timed launches, mean of the HIP-event times) and steady state (after 0.25 s of back-to-back
 launches, 100 launches). Streams of both forms are compared with each other (the GPU parity tests compare them with
 the oracle). One JSON line per case."""
@@ -40,6 +40,9 @@ def steady(fn):
     return timed(fn, 0, 100)[0]
 
 
+FORMS = ("tile", "range", "single_pass")  # default (tile count + scan + placed tile coder), k_encode1d_var, look-back
+
+
 def main():
     n = 256 << 20
     x32 = torch.empty(n, dtype=torch.float32, device="cuda")
@@ -54,11 +57,13 @@ def main():
         res = {"case": name}
         streams = {}
         for rnd in range(2):
-            for form in ("single_pass", "two_pass"):
-                if form == "two_pass":
-                    os.environ["GCOW_VAR1D_TWO_PASS"] = "1"
-                else:
-                    os.environ.pop("GCOW_VAR1D_TWO_PASS", None)
+            for form in FORMS:
+                os.environ.pop("GCOW_VAR1D_SINGLE_PASS", None)
+                os.environ.pop("GCOW_VAR1D_FORM", None)
+                if form == "single_pass":
+                    os.environ["GCOW_VAR1D_SINGLE_PASS"] = "1"
+                elif form == "range":
+                    os.environ["GCOW_VAR1D_FORM"] = "range"
                 cold, per = timed(lambda: enc(x), 5, 20)
                 st = steady(lambda: enc(x))
                 e = enc(x)
@@ -75,10 +80,11 @@ def main():
                     streams[form] = (bits, e.stream().clone())
                 res.setdefault(form, []).append({"cold_ms": round(cold, 4), "first_ms": round(per[0], 4),
                                                  "steady_ms": round(st, 4)})
-        os.environ.pop("GCOW_VAR1D_TWO_PASS", None)
-        res["bits_per_value"] = round(streams["single_pass"][0] / n, 3)
-        res["streams_equal"] = (streams["single_pass"][0] == streams["two_pass"][0] and
-                                torch.equal(streams["single_pass"][1], streams["two_pass"][1]))
+        os.environ.pop("GCOW_VAR1D_SINGLE_PASS", None)
+        os.environ.pop("GCOW_VAR1D_FORM", None)
+        s0 = streams[FORMS[0]]
+        res["bits_per_value"] = round(s0[0] / n, 3)
+        res["streams_equal"] = all(s0[0] == streams[f][0] and torch.equal(s0[1], streams[f][1]) for f in FORMS[1:])
         print(json.dumps(res), flush=True)
         del enc, streams
         torch.cuda.empty_cache()

@@ -8,6 +8,7 @@ import time
 
 import torch
 
+os.environ.setdefault("GCOW_VAR1D_SINGLE_PASS", "1")  # the single-pass form (the ablation builds' kernel)
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 if "--lib" in sys.argv:
