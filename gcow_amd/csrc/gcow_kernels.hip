@@ -218,11 +218,7 @@ __device__ __forceinline__ uint64_t encode_block1d_lean5(const float* f, const u
 //  * the group-phase end jg = clz(u2 | u3) - sh, with 31 for o23 = 0 (jg = M0);
 //  * zero blocks coded by the main path (u = 0 codes to all-zero bits after a zero header), so only tiny-normal and
 //    subnormal maxima (0 < E < 29) take the constant payload.
-//  * W24 (lean-7): one 24-plane window (12 lookups, bitop3 ORs) instead of 16 planes plus a second 16-plane window
-//    behind a wave vote: 24 planes always reach the budget at WB = 64 -- the group phase's j <= 16 planes cost >= 2 bits
-//    each, so plane 16 lands at p2 >= 9 + 2 j + 4 (16 - j) >= 41 and plane 24 at >= 73; planes below plane 0 are the
-//    zeros shifted into w, which is the zero padding of the budget.
-template <uint32_t WB, bool W2LOW = false, bool W24 = false>
+template <uint32_t WB, bool W2LOW = false>
 __device__ __forceinline__ uint64_t encode_block1d_lean6(const float* f, const uint32_t* tab, const uint32_t* rs,
                                                          bool& special)
 {
@@ -249,8 +245,7 @@ __device__ __forceinline__ uint64_t encode_block1d_lean6(const float* f, const u
   const int M0 = 31 - (int)sh;
   const int jg = (int)min(ffbh_hw(o23), 31u) - (int)sh;  // group phase: window nibbles 0 .. jg (o23 = 0: M0)
   const uint32_t w0 = u0 << sh, w1 = u1 << sh, w2 = u2 << sh, w3 = u3 << sh;
-  uint32_t Y3 = 0;
-  const uint64_t Y = W24 ? window_lds24(rs, w0, w1, w2, w3, Y3) : window_lds(rs, w0, w1, w2, w3);
+  const uint64_t Y = window_lds(rs, w0, w1, w2, w3);
   uint32_t pos = 9 + sh;
   uint32_t e = tab[(uint32_t)Y & 255u];
   uint32_t G = e >> 17, gl = (e >> 13) & 15u;
@@ -277,9 +272,7 @@ __device__ __forceinline__ uint64_t encode_block1d_lean6(const float* f, const u
   special = special || (!tiny && jg >= 16 && pos < WB);  // group phase runs past the 16-plane window
   if (j < 16 && pos < WB) acc |= (Y >> (4 * j)) << pos;  // rest of the window, verbatim
   const uint32_t p2 = pos + 4u * (uint32_t)(16 - j);      // where plane M0 - 16 lands
-  if constexpr (W24) {
-    if (p2 < WB) acc |= (uint64_t)Y3 << p2;
-  } else if (__any(p2 < WB && M0 >= 16)) {
+  if (__any(p2 < WB && M0 >= 16)) {
     uint64_t Y2;  // planes M0-16 .. M0-31
     if constexpr (W2LOW) {
       Y2 = window_lds_low(rs, w0, w1, w2, w3);
@@ -414,7 +407,7 @@ __global__ __launch_bounds__(T) void k_encode_fixed1d_np(const void* __restrict_
     float f[4];
     PipeRow<DT>::unpack(r[k], f);
     bool special;
-    uint64_t w = encode_block1d_lean6<WB, (V & 2) != 0, (V & 4) != 0>(f, tab, tab + 1280, special);
+    uint64_t w = encode_block1d_lean6<WB, (V & 2) != 0>(f, tab, tab + 1280, special);
     if (special) {
       RegWriter64 rw{0ull, 0u};
       encode_block<1>(rw, f, p);
@@ -2076,13 +2069,6 @@ __global__ void k_fill_normal(float* __restrict__ out, uint64_t count, double si
 // ------------------------------------------------------------------------------------------------ launchers
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
-// GCOW_FIXED1D_LEAN=6 (A/B): the lean-6 coder (16-plane window + a second one behind a wave vote); default lean-7
-static int fixed1d_variant()
-{
-  const char* e = getenv("GCOW_FIXED1D_LEAN");
-  return e && e[0] == '6' ? 6 : 7;
-}
-
 template <int DT, uint32_t WB>
 static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, void* out, hipStream_t st)
 {
@@ -2100,8 +2086,7 @@ static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, vo
         const uint32_t nc = min(CH, nfull - c0);
         const void* ic = (const char*)in + (size_t)c0 * IB;
         void* oc = (char*)out + (size_t)c0 * (WB / 8);
-        if (fixed1d_variant() == 6) k_encode_fixed1d_np<DT, WB, 8, 256, 3><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
-        else k_encode_fixed1d_np<DT, WB, 8, 256, 7><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
+        k_encode_fixed1d_np<DT, WB, 8, 256, 3><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
       }
     }
   }

@@ -202,25 +202,6 @@ __device__ __forceinline__ uint64_t window_lds(const uint32_t* rs, uint32_t w0, 
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-// a | b | c | d with one v_bitop3_b32 (issues like a plain v_or_b32 on gfx950; v_or3_b32 takes 1.65x as long,
-// profiles/r02_valu_issue_rates.log)
-__device__ __forceinline__ uint32_t or4(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
-{
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xfe) | d;
-}
-
-// 24 planes from plane 31 of w down: nibbles 0..15 as Y (bytes 3 and 2 of w), nibbles 16..23 as y3 (byte 1).
-__device__ __forceinline__ uint64_t window_lds24(const uint32_t* rs, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
-                                                 uint32_t& y3)
-{
-  const uint32_t lo = or4(rs[w0 >> 24], rs[256 + (w1 >> 24)], rs[512 + (w2 >> 24)], rs[768 + (w3 >> 24)]);
-  const uint32_t hi = or4(rs[(w0 >> 16) & 255u], rs[256 + ((w1 >> 16) & 255u)], rs[512 + ((w2 >> 16) & 255u)],
-                          rs[768 + ((w3 >> 16) & 255u)]);
-  y3 = or4(rs[(w0 >> 8) & 255u], rs[256 + ((w1 >> 8) & 255u)], rs[512 + ((w2 >> 8) & 255u)],
-           rs[768 + ((w3 >> 8) & 255u)]);
-  return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-
 // planes 16..31 below the top of w (bytes 1 and 0 of the same shifted words): the second window
 __device__ __forceinline__ uint64_t window_lds_low(const uint32_t* rs, uint32_t w0, uint32_t w1, uint32_t w2,
                                                    uint32_t w3)
