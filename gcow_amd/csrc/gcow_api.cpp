@@ -772,9 +772,10 @@ size_t gcow_encode_workspace_bytes(const zfp_input* field, const gcow_params* p)
   // sums, base; 3-D variable rate also keeps every block's length (uint16) from the count pass for the encode pass
   const size_t lens = F.dims == 3 ? ((size_t)F.nblocks * 2 + 7) / 8 * 8 : 0;
   const size_t two_pass = (2 * (size_t)pl.nranges + 1) * 8 + lens;
-  // 1-D variable rate without a budget: the single-pass encoder's look-back status and boundary words
+  // 1-D variable rate without a budget: the tile form's tile sums, offsets and byte lengths (the default), or the
+  // single-pass encoder's look-back status and boundary words
   if (F.dims == 1 && pl.threads == 256 && p->minbits <= 1 && p->maxbits >= 160)
-    return std::max(two_pass, gcow::var1d_sp_workspace_bytes(F.nblocks));
+    return std::max({two_pass, gcow::var1d_sp_workspace_bytes(F.nblocks), gcow::var1d_tile_workspace_bytes(F.nblocks)});
   return two_pass;
 }
 

@@ -2148,18 +2148,10 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
   if (var1d && single && single[0] == '1')
     return launch_encode1d_var_sp(F, p, out32, ws_sums, d_total, index, index_shift, d_base, st);
   // GCOW_VAR1D_FORM=range (A/B, tests): the count + scan + k_encode1d_var form over ranges of plan.range blocks.
-  // Default: count per tile of var1d_tile_blocks() blocks, scan, and the single-pass encoder's tile kernel placed by
-  // the scan (its coder: lane accumulators, no LDS atomics; the workspace holds 2 ntiles + 1 words,
-  // var1d_sp_workspace_bytes)
+  // Default: the tile form (var1d.hip: count per tile with byte lengths, scan, the tile coder placed by the scan)
   const char* form = getenv("GCOW_VAR1D_FORM");
-  if (var1d && !(form && form[0] == 'r')) {
-    const uint32_t tb = var1d_tile_blocks();
-    const uint32_t ntiles = (uint32_t)((F.nblocks + tb - 1) / tb);
-    uint64_t* base = ws_sums + ntiles;
-    k_count1d_var<DT, 4><<<ntiles, T, 0, st>>>(F, p, tb, ws_sums);
-    scan_ranges(ws_sums, ntiles, base, d_total, out32, d_base, st);
-    return launch_encode1d_var_placed(F, p, out32, base, index, index_shift, st);
-  }
+  if (var1d && !(form && form[0] == 'r'))
+    return launch_encode1d_var_tile(F, p, out32, ws_sums, d_total, index, index_shift, d_base, st);
   if (var1d) k_count1d_var<DT, 4><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   else k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   scan_ranges(ws_sums, plan.nranges, ws_base, d_total, out32, d_base, st);

@@ -72,11 +72,12 @@ size_t var1d_sp_workspace_bytes(uint64_t nblocks);
 hipError_t launch_encode1d_var_sp(const FieldDesc& F, const Params& p, uint32_t* out32, uint64_t* ws,
                                   uint64_t* d_total, uint64_t* index, uint32_t index_shift, const uint64_t* d_base,
                                   void* stream);
-// The same tile kernel placed by a scan instead of the look-back: rbase[t] = stream bit offset of tile t (V1TILE blocks)
-// from k_count1d_var (range = var1d_tile_blocks()) + launch_scan_ranges, which also zeroed the words tiles share.
-uint32_t var1d_tile_blocks();
-hipError_t launch_encode1d_var_placed(const FieldDesc& F, const Params& p, uint32_t* out32, const uint64_t* rbase,
-                                      uint64_t* index, uint32_t index_shift, void* stream);
+// The default 1-D variable-rate form (var1d.hip): count per tile + scan + the tile coder placed by the scan;
+// ws = var1d_tile_workspace_bytes().
+size_t var1d_tile_workspace_bytes(uint64_t nblocks);
+hipError_t launch_encode1d_var_tile(const FieldDesc& F, const Params& p, uint32_t* out32, uint64_t* ws,
+                                    uint64_t* d_total, uint64_t* index, uint32_t index_shift, const uint64_t* d_base,
+                                    void* stream);
 hipError_t launch_copy_pattern1d(const void* in, int dtype, uint64_t nvals, uint32_t wb, void* out, void* stream);
 // *flag = 0, then 1 if a[i] != b[i] for any i < n
 hipError_t launch_words_differ(const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t* flag, void* stream);

@@ -247,7 +247,7 @@ __device__ __forceinline__ void v1_prepare(const FieldDesc& F, const Params& p, 
     lsum += T.len[k];
   }
   T.excl = block_exclusive_scan<V1T>(lsum, &T.total, scan_sh);
-  if (status && threadIdx.x == 0)  // incl_base given (tile 0): the inclusive prefix at once
+  if (threadIdx.x == 0)  // incl_base given (tile 0): the inclusive prefix at once
     __hip_atomic_store(status + t, incl_base != ~0ull ? ((2ull << 62) | (incl_base + T.total)) : ((1ull << 62) | T.total),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -353,16 +353,13 @@ __device__ uint64_t v1_lookback(uint64_t* status, uint32_t t, uint64_t base0, co
 // lanes' offsets by a workgroup scan) and publish its total at once; code into the LDS window at tile-relative
 // positions; look back (one wave) for the stream offset; store the window shifted to the offset, the two words shared
 // with the neighbouring tiles through v1_boundary.
-// LB = false: the tile's offset is rbase[t] from a count pass and a scan (no status words; the scan zeroed the words
-// two tiles share, so both contributors atomicOr them into the stream).
-template <int DT, bool LB = true>
+template <int DT>
 __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, uint64_t* __restrict__ status,
                                                          uint64_t* __restrict__ bnd, uint32_t* __restrict__ out32,
                                                          uint64_t* __restrict__ index, uint32_t index_shift,
                                                          const uint64_t* __restrict__ d_base,
                                                          uint64_t* __restrict__ d_total, uint32_t ntiles,
-                                                         uint32_t spin, uint64_t* __restrict__ stats,
-                                                         const uint64_t* __restrict__ rbase = nullptr)
+                                                         uint32_t spin, uint64_t* __restrict__ stats)
 {
   __shared__ uint32_t tab[1280];  // pair table (lean-5 entries, rows n >= 3 empty)
   __shared__ uint32_t rs[1024];   // window spread tables
@@ -377,11 +374,11 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, 
   for (uint32_t i = tid; i < 1024; i += V1T) rs[i] = rspread_entry(i);
   if (tid == 0) s_special = 0;
   const bool wide_ok = F.vec && (((uintptr_t)F.data) & 15u) == 0;
-  const uint64_t base0 = LB && d_base ? *d_base : 0ull;
+  const uint64_t base0 = d_base ? *d_base : 0ull;
   V1Raw<DT> raw;
   raw.load(F, t, wide_ok);
   V1Tile T;
-  v1_prepare<DT>(F, p, raw, t, T, scan_sh, LB ? status : nullptr, t == 0 ? base0 : ~0ull);
+  v1_prepare<DT>(F, p, raw, t, T, scan_sh, status, t == 0 ? base0 : ~0ull);
   const uint32_t excl = T.excl, total = T.total;
   uint32_t lsum = 0;
 #pragma unroll
@@ -455,9 +452,7 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, 
   }
 
   // ---- the tile's stream offset (wave 0)
-  if (!LB) {
-    if (tid == 0) s_base = rbase[t];
-  } else if (tid < 64) {
+  if (tid < 64) {
     const uint64_t B = t == 0 ? base0
                               : ((V1_ABLATE & 1) ? (uint64_t)t << 16
                                                  : v1_lookback<DT>(status, t, base0, F, p, lane, spin, stats));
@@ -492,9 +487,7 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, 
     uint32_t* dst = out32 + g0 + k;
     const bool first = k == 0 && rb != 0;
     const bool tail = k == nw - 1 && ((rb + total) & 31u) != 0 && !last_tile;
-    if (!LB && (first || tail)) {
-      atomicOr(dst, val);  // a word shared with a neighbouring tile (zeroed by the scan) or the appended stream
-    } else if (first) {
+    if (first) {
       if (t == 0) atomicOr(dst, val);  // bits already in the stream before d_base (append)
       else v1_boundary(bnd, t - 1, 1u, dst, val);
     } else if (tail) {
@@ -542,19 +535,203 @@ hipError_t launch_encode1d_var_sp(const FieldDesc& F, const Params& p, uint32_t*
   return hipGetLastError();
 }
 
-uint32_t var1d_tile_blocks() { return V1TILE; }
+// ------------------------------------------------------------------------------------------------ tile form (default)
+// count + scan + placed tile coder. The look-back above waits on predecessors spread over the eight XCDs (C5: 0.91 ms
+// against 0.71 ms for this form, profiles/r03_c5_forms_ab.log); here the offsets come from a scan instead:
+//   k_count1d_var_tile   one tile of V1TILE blocks per workgroup: every block's length (closed form, v1_prep) as a
+//                        byte (lens8: one 32-bit word per lane, its V1U blocks) and the tile's total (sums[t]);
+//   k_scan_ranges(_mw)   the tiles' stream offsets (base), zeroing the words two tiles share;
+//   k_encode1d_var_tile  the lane's offset in the tile by a workgroup scan of the stored lengths (before any block is
+//                        prepared, so prepare and code run per block, the coefficients live only for one block), the
+//                        blocks coded at their bit position relative to the tile's first stream word (base & 31 + the
+//                        lane offset) into the LDS window through the lane accumulator, and the window stored as
+//                        whole 32-bit stream words (no shifting; the two words shared with the neighbours by atomicOr).
+template <int DT>
+__global__ __launch_bounds__(V1T) void k_count1d_var_tile(FieldDesc F, Params p, uint64_t* __restrict__ sums,
+                                                          uint32_t* __restrict__ lens8)
+{
+  __shared__ uint32_t red[V1T / 64];
+  const uint32_t tid = threadIdx.x, t = blockIdx.x;
+  const bool wide_ok = F.vec && (((uintptr_t)F.data) & 15u) == 0;
+  V1Raw<DT> raw;
+  raw.load(F, t, wide_ok);
+  const uint64_t bl = (uint64_t)t * V1TILE + (uint64_t)tid * V1U;
+  uint32_t packed = 0, lsum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < V1U; k++) {
+    float f[4];
+    raw.block(k, f);
+    uint32_t u[4], hdr, K;
+    bool inf;
+    uint32_t len = v1_prep(f, -122 - p.minexp, (int)min(p.maxprec, 64u), u, hdr, K, inf);
+    const bool valid = bl + k < F.nblocks;
+    if (inf && valid) len = count_block<1>(f, p);
+    len = valid ? len : 0u;  // <= 140
+    packed |= len << (8 * k);
+    lsum += len;
+  }
+  lens8[(size_t)t * V1T + tid] = packed;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
+  if ((tid & 63u) == 0) red[tid >> 6] = lsum;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < V1T / 64; w++) tot += red[w];
+    sums[t] = tot;
+  }
+}
 
-hipError_t launch_encode1d_var_placed(const FieldDesc& F, const Params& p, uint32_t* out32, const uint64_t* rbase,
-                                      uint64_t* index, uint32_t index_shift, void* stream)
+template <int DT>
+__global__ __launch_bounds__(V1T) void k_encode1d_var_tile(FieldDesc F, Params p, const uint64_t* __restrict__ rbase,
+                                                           const uint32_t* __restrict__ lens8,
+                                                           uint32_t* __restrict__ out32, uint64_t* __restrict__ index,
+                                                           uint32_t index_shift, uint32_t ntiles)
+{
+  __shared__ uint32_t tab[1280];  // pair table (lean-5 entries, rows n >= 3 empty)
+  __shared__ uint32_t rs[1024];   // window spread tables
+  __shared__ uint64_t win[V1Q];   // the tile's code from bit (base & 31) of its first stream word
+  __shared__ uint32_t scan_sh[V1T / 64];
+  __shared__ uint32_t s_special;
+  uint32_t* win32 = (uint32_t*)win;
+  const uint32_t tid = threadIdx.x, t = blockIdx.x;
+  for (uint32_t i = tid; i < 1280; i += V1T) tab[i] = g_plane_tab_var.v[i];
+  for (uint32_t i = tid; i < 1024; i += V1T) rs[i] = rspread_entry(i);
+  if (tid == 0) s_special = 0;
+  const bool wide_ok = F.vec && (((uintptr_t)F.data) & 15u) == 0;
+  V1Raw<DT> raw;
+  raw.load(F, t, wide_ok);
+  const uint32_t lw = lens8[(size_t)t * V1T + tid];
+  const uint64_t B = rbase[t];
+  const uint32_t lb = (uint32_t)(B & 31u);
+  uint32_t len[V1U], lsum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < V1U; k++) {
+    len[k] = (lw >> (8 * k)) & 255u;
+    lsum += len[k];
+  }
+  uint32_t total;
+  const uint32_t excl = lb + block_exclusive_scan<V1T>(lsum, &total, scan_sh);
+  if (lsum) {  // the two words this lane shares with its neighbours start at zero (lane 0: the bits below lb too)
+    win[excl >> 6] = 0ull;
+    win[(excl + lsum - 1) >> 6] = 0ull;
+  }
+  __syncthreads();
+
+  // ---- prepare and code the lane's blocks one at a time: a 64-bit accumulator; whole words are plain LDS stores,
+  // the two shared ones ds_or
+  const uint64_t bl = (uint64_t)t * V1TILE + (uint64_t)tid * V1U;
+  const int cexp = -122 - p.minexp, maxprec = (int)min(p.maxprec, 64u);
+  uint64_t acc = 0;
+  uint32_t q = excl >> 6, fill = excl & 63u;
+  const uint32_t qhead = q;
+  uint32_t spmask = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < V1U; k++) {
+    float f[4];
+    raw.block(k, f);
+    uint32_t u[4], hdr, K;
+    bool inf;
+    (void)v1_prep(f, cexp, maxprec, u, hdr, K, inf);  // the length comes from the count pass
+    bool sp = inf && bl + k < F.nblocks;
+    uint64_t c0, c1;
+    v1_code(u, hdr, len[k], K, tab, rs, c0, c1, sp);
+    sp = sp && len[k];
+    if (sp) c0 = c1 = 0ull;  // coded below by the generic coder, OR-ed into these zero bits
+    spmask |= (uint32_t)sp << k;
+    acc |= c0 << fill;
+    const uint64_t mid = ((c0 >> 1) >> (63u - fill)) | (c1 << fill);
+    const uint64_t hi = (c1 >> 1) >> (63u - fill);
+    const uint32_t nf = fill + len[k];
+    if (nf >= 64u) {
+      if (q == qhead) atomicOr((unsigned long long*)&win[q], (unsigned long long)acc);
+      else win[q] = acc;
+      q++;
+      acc = mid;
+      if (nf >= 128u) {
+        win[q] = acc;
+        q++;
+        acc = hi;
+        if (nf >= 192u) {  // a special block of up to 140 bits (its code is zero here) completes a third word
+          win[q] = acc;
+          q++;
+          acc = 0ull;
+        }
+      }
+    }
+    fill = nf & 63u;
+    acc &= (1ull << fill) - 1ull;
+  }
+  if (fill) atomicOr((unsigned long long*)&win[q], (unsigned long long)acc);
+  if (spmask) s_special = 1u;
+  __syncthreads();
+  if (s_special) {  // Inf / NaN blocks, long group phases, codes past 128 bits: the generic coder
+    uint32_t o = excl;
+#pragma unroll
+    for (uint32_t k = 0; k < V1U; k++) {
+      if ((spmask >> k) & 1u) {
+        float f[4];
+        raw.block(k, f);
+        LdsWriter wr{win32, o, o + len[k]};
+        encode_block<1>(wr, f, p);
+      }
+      o += len[k];
+    }
+    __syncthreads();
+  }
+  if (index) {
+    uint32_t o = excl;
+#pragma unroll
+    for (uint32_t k = 0; k < V1U; k++) {
+      const uint64_t b = bl + k;
+      if (len[k] && (b & ((1ull << index_shift) - 1ull)) == 0) index[b >> index_shift] = B - lb + o;
+      o += len[k];
+    }
+  }
+
+  // ---- store the window: whole 32-bit stream words from word B >> 5, coalesced
+  const uint64_t g0 = B >> 5;
+  const uint32_t nw = (lb + total + 31u) >> 5;
+  const bool last_tile = t == ntiles - 1;
+  const bool tail_shared = ((lb + total) & 31u) != 0 && !last_tile;
+  for (uint32_t k = tid; k < nw; k += V1T) {
+    const uint32_t val = win32[k];
+    if ((k == 0 && lb != 0) || (k == nw - 1 && tail_shared)) atomicOr(out32 + g0 + k, val);
+    else out32[g0 + k] = val;
+  }
+  if (last_tile && tid == 0) {
+    const uint64_t endw = (B + total + 31) >> 5;
+    if (endw & 1) out32[endw] = 0u;  // stream_flush: zero-pad to a 64-bit boundary (stream.c:132-138)
+  }
+}
+
+// The tile form's workspace: sums[ntiles], base[ntiles + 1] (uint64), then the byte lengths of whole tiles.
+size_t var1d_tile_workspace_bytes(uint64_t nblocks)
+{
+  const uint64_t ntiles = (nblocks + V1TILE - 1) / V1TILE;
+  return (size_t)((2 * ntiles + 2) * 8 + ntiles * V1TILE);
+}
+
+hipError_t launch_encode1d_var_tile(const FieldDesc& F, const Params& p, uint32_t* out32, uint64_t* ws,
+                                    uint64_t* d_total, uint64_t* index, uint32_t index_shift, const uint64_t* d_base,
+                                    void* stream)
 {
   hipStream_t st = (hipStream_t)stream;
   const uint32_t ntiles = (uint32_t)((F.nblocks + V1TILE - 1) / V1TILE);
+  uint64_t* sums = ws;
+  uint64_t* base = ws + ntiles;
+  uint32_t* lens8 = (uint32_t*)(ws + 2 * (size_t)ntiles + 2);
+  if (F.dtype == DT_BF16) k_count1d_var_tile<DT_BF16><<<ntiles, V1T, 0, st>>>(F, p, sums, lens8);
+  else k_count1d_var_tile<DT_F32><<<ntiles, V1T, 0, st>>>(F, p, sums, lens8);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = launch_scan_ranges(sums, ntiles, base, d_total, out32, d_base, st);
+  if (e != hipSuccess) return e;
   if (F.dtype == DT_BF16)
-    k_encode1d_var_sp<DT_BF16, false><<<ntiles, V1T, 0, st>>>(F, p, nullptr, nullptr, out32, index, index_shift,
-                                                              nullptr, nullptr, ntiles, 0, nullptr, rbase);
+    k_encode1d_var_tile<DT_BF16><<<ntiles, V1T, 0, st>>>(F, p, base, lens8, out32, index, index_shift, ntiles);
   else
-    k_encode1d_var_sp<DT_F32, false><<<ntiles, V1T, 0, st>>>(F, p, nullptr, nullptr, out32, index, index_shift,
-                                                             nullptr, nullptr, ntiles, 0, nullptr, rbase);
+    k_encode1d_var_tile<DT_F32><<<ntiles, V1T, 0, st>>>(F, p, base, lens8, out32, index, index_shift, ntiles);
   return hipGetLastError();
 }
 
