@@ -41,39 +41,31 @@ constexpr uint32_t V1MAXB = 140;                             // 9 + 3 + 4 * 32: 
 constexpr uint32_t V1Q = (V1TILE * V1MAXB + 63) / 64 + 2;    // LDS window, 64-bit words
 constexpr uint64_t V1VAL = (1ull << 62) - 1;                 // status word: flag << 62 | value
 // V1_ABLATE (measurement builds only, tools/ubench/var1d_ablate.sh; 0 in the product): 1 = no look-back (tile t at
-// t * 64 Ki bits), 2 = no coding (zero codes, lengths kept), 4 = no window store, 8 = no pair loop
+// t * 64 Ki bits), 2 = no coding (zero codes / prepared words, lengths kept), 4 = no window store, 8 = no pair loop,
+// 16 = no prepare in the tile coder (raw words as coefficients), 32 = no length computation in the tile count
 #ifndef V1_ABLATE
 #define V1_ABLATE 0
 #endif
 constexpr uint32_t V1SPIN = 96;  // polls (~1.5 us each) of a missing predecessor before computing its total here
 
-// Negabinary coefficients of a block whose four values cast to INT_MIN (emax <= -98: the scale 2^(30 - emax)
-// overflows to +inf; x86 cvttss2si of +-inf and NaN is INT_MIN, encode.c:162-187): the lift (encode.c:212-225) and
-// map (encode.c:263-275) of four INT_MIN.
-struct TinyU {
-  uint32_t v[4];
-};
-__host__ __device__ constexpr TinyU make_tiny_u()
+// v_lshlrev_b32 as an opaque instruction: the shift count's low 5 bits (a count of 32 shifts by 0, not UB)
+__device__ __forceinline__ uint32_t shl_hw(uint32_t x, uint32_t n)
 {
-  auto asr = [](uint32_t v) { return (v >> 1) | (v & 0x80000000u); };
-  uint32_t x = 0x80000000u, y = x, z = x, w = x;
-  x += w; x = asr(x); w -= x;
-  z += y; z = asr(z); y -= z;
-  x += z; x = asr(x); z -= x;
-  w += y; w = asr(w); y -= w;
-  w += asr(y); y -= asr(w);
-  constexpr uint32_t NB = 0xaaaaaaaau;
-  return TinyU{{(x + NB) ^ NB, (y + NB) ^ NB, (z + NB) ^ NB, (w + NB) ^ NB}};
+  uint32_t r;
+  asm("v_lshlrev_b32 %0, %1, %2" : "=v"(r) : "v"(n), "v"(x));
+  return r;
 }
-constexpr TinyU kTinyU = make_tiny_u();
 
 // The lean-5 pair table with its rows n = 3 and 4 emptied (no bits, the row kept): from n = 3 on every plane is its
 // nibble verbatim (encode.c:301-333 with one coefficient left), which the variable-rate coder takes from the window
 // instead, so a lane whose group phase is over adds nothing more -- no per-lane selects in the pair loop.
+// Row n' = 4 is folded into row 3 (both are empty), so the tile kernels keep only rows 0..3 (4 KB) in LDS.
 __host__ __device__ constexpr PlaneTab2 make_plane_tab_var()
 {
   PlaneTab2 T = make_plane_tab5();
-  for (uint32_t t = 3 * 256; t < 1280; t++) T.v[t] = (t >> 8) << 10;
+  for (uint32_t t = 0; t < 3 * 256; t++)
+    if ((T.v[t] & 0x1c00u) == (4u << 10)) T.v[t] = (T.v[t] & ~0x1c00u) | (3u << 10);
+  for (uint32_t t = 3 * 256; t < 1280; t++) T.v[t] = 3u << 10;
   return T;
 }
 __device__ const PlaneTab2 g_plane_tab_var = make_plane_tab_var();
@@ -93,9 +85,12 @@ __device__ __forceinline__ uint32_t v1_prep(const float* f, int cexp, int maxpre
   // get_precision, d = 1 (common.c:226-229); subnormal maxima clamp emax to -126 (encode.c:142-152)
   const int prec = min(max((int)E + cexp, 0), maxprec);
   K = (uint32_t)min(max(prec - 1, 0), 31);
-  const float s = __uint_as_float(0x8d800000u - (m & 0x7f800000u));  // 2^(30 - emax); tiny blocks replaced below
-  uint32_t x = (uint32_t)cvt_i32_hw(f[0] * s), y = (uint32_t)cvt_i32_hw(f[1] * s);
-  uint32_t z = (uint32_t)cvt_i32_hw(f[2] * s), w = (uint32_t)cvt_i32_hw(f[3] * s);
+  const float s = __uint_as_float(0x8d800000u - (m & 0x7f800000u));  // 2^(30 - emax)
+  // every value of a block with E < 29 casts to INT_MIN (the scale overflows; x86 cvttss2si, encode.c:162-187):
+  // an integer mask selects it per value (v_bfi), no compare-to-mask selects
+  const uint32_t tm = (uint32_t)((int32_t)(E - 29u) >> 31);
+  auto cast = [&](float v) { return ((uint32_t)cvt_i32_hw(v * s) & ~tm) | (tm & 0x80000000u); };
+  uint32_t x = cast(f[0]), y = cast(f[1]), z = cast(f[2]), w = cast(f[3]);
   auto asr = [](uint32_t v) { return (uint32_t)((int32_t)v >> 1); };
   constexpr uint32_t NB = 0xaaaaaaaau;
   x = asr(x + w); w -= x;  // fwd_lift (encode.c:212-225), int32 wraparound
@@ -107,25 +102,19 @@ __device__ __forceinline__ uint32_t v1_prep(const float* f, int cexp, int maxpre
   u[1] = (y + NB) ^ NB;
   u[2] = (z + NB) ^ NB;
   u[3] = (w + NB) ^ NB;
-  if (__any(E < 29u)) {  // every value casts to INT_MIN (or the block is zero): rare, so a wave-uniform branch
-    if (E < 29u) {
-      u[0] = kTinyU.v[0];
-      u[1] = kTinyU.v[1];
-      u[2] = kTinyU.v[2];
-      u[3] = kTinyU.v[3];
-    }
-  }
   const bool one = m == 0 || prec == 0;  // a single 0 bit (encode.c:471-475)
   hdr = one ? 0u : 2u * E + 3u;
-  // encode_ints' length from the leading planes (codec_device.h encode_ints_length, B = 4), with the count c of
-  // coefficients significant at kmin folded in: 1 + 4 K + sum_{j<3} (on_j - min(z_j, K) + [on_j and L_j = R_j])
+  // encode_ints' length from the leading planes (codec_device.h encode_ints_length, B = 4), integer-only:
+  //   4 + 4 K - sum_{j<3} c_j + sum_{j<3} e_j,  c_j = min(z_j, K + 1), z_j = ffbh(S_j) of the suffix OR S_j,
+  //   e_j = [c_j <= K and bit 31 - z_j of u_j is set] (L_j = R_j: u_j holds the leading plane of S_j)
+  // (the c = 4 case of the general form folded in; tests/test_length_formula.py checks it against the oracle)
   const uint32_t S2 = u[2] | u[3], S1 = u[1] | S2, S0 = u[0] | S1;
-  const uint32_t z2 = ffbh_hw(S2), z1 = ffbh_hw(S1), z0 = ffbh_hw(S0);
-  const bool on2 = z2 <= K, on1 = z1 <= K, on0 = z0 <= K;
-  uint32_t len = 1u + 4u * K - (min(z2, K) + min(z1, K) + min(z0, K));
-  len += (uint32_t)on0 + (uint32_t)on1 + (uint32_t)on2;
-  len += (uint32_t)(on2 && (u[2] ^ S2) < u[2]) + (uint32_t)(on1 && (u[1] ^ S1) < u[1]) +
-         (uint32_t)(on0 && (u[0] ^ S0) < u[0]);
+  const uint32_t K1 = K + 1u;
+  const uint32_t c2 = min(ffbh_hw(S2), K1), c1 = min(ffbh_hw(S1), K1), c0 = min(ffbh_hw(S0), K1);
+  const uint32_t e2 = (shl_hw(u[2], c2) >> 31) & min(K1 - c2, 1u);  // c_j = 32 (K = 31, S_j = 0): e_j = 0
+  const uint32_t e1 = (shl_hw(u[1], c1) >> 31) & min(K1 - c1, 1u);
+  const uint32_t e0 = (shl_hw(u[0], c0) >> 31) & min(K1 - c0, 1u);
+  const uint32_t len = 4u + 4u * K - (c0 + c1 + c2) + (e0 + e1 + e2);
   return one ? 1u : 9u + len;
 }
 
@@ -538,85 +527,182 @@ hipError_t launch_encode1d_var_sp(const FieldDesc& F, const Params& p, uint32_t*
 // ------------------------------------------------------------------------------------------------ tile form (default)
 // count + scan + placed tile coder. The look-back above waits on predecessors spread over the eight XCDs (C5: 0.91 ms
 // against 0.71 ms for this form, profiles/r03_c5_forms_ab.log); here the offsets come from a scan instead:
-//   k_count1d_var_tile   one tile of V1TILE blocks per workgroup: every block's length (closed form, v1_prep) as a
-//                        byte (lens8: one 32-bit word per lane, its V1U blocks) and the tile's total (sums[t]);
+//   k_count1d_var_tile   V1CT tiles of V1TILE blocks per workgroup, the next tile's loads issued before a tile is counted:
+//                        each block's length (closed form, v1_prep) as a byte (lens8: one 32-bit word per lane and
+//                        tile, its V1U blocks) and each tile's total (sums[t]);
 //   k_scan_ranges(_mw)   the tiles' stream offsets (base), zeroing the words two tiles share;
-//   k_encode1d_var_tile  the lane's offset in the tile by a workgroup scan of the stored lengths (before any block is
-//                        prepared, so prepare and code run per block, the coefficients live only for one block), the
-//                        blocks coded at their bit position relative to the tile's first stream word (base & 31 + the
-//                        lane offset) into the LDS window through the lane accumulator, and the window stored as
-//                        whole 32-bit stream words (no shifting; the two words shared with the neighbours by atomicOr).
-template <int DT>
-__global__ __launch_bounds__(V1T) void k_count1d_var_tile(FieldDesc F, Params p, uint64_t* __restrict__ sums,
-                                                          uint32_t* __restrict__ lens8)
+//   k_encode1d_var_tile  one tile per workgroup: the lane's offset in the tile by a workgroup scan of the stored
+//                        lengths (before any block is prepared, so prepare and code run per block and the
+//                        coefficients live only for one block), the blocks coded at their bit position relative to the
+//                        16-byte stream boundary below the tile (base & 127 + the lane offset) into an LDS window
+//                        through the lane accumulator, and the window stored as 16-byte chunks of stream words (no
+//                        shifting; the two words shared with the neighbours by atomicOr). The window holds V1QS qwords (95 bits per block on
+//                        average) so that 8 workgroups fit a CU (the kernel waits on memory and LDS latency: occupancy,
+//                        not VALU issue, bounds it); a tile that needs more is skipped and coded by
+//   k_encode1d_var_tile_big  the same body with the worst-case window (140 bits per block), a grid-stride loop over
+//                        the list of oversized tiles k_encode1d_var_tile appended to (the count kernel empties it).
+constexpr uint32_t V1CT = 8;                                      // tiles per count workgroup
+constexpr uint32_t V1QS = 1500;                                   // small window, qwords
+constexpr uint32_t V1TAB = 1024;                                  // pair-table rows 0..3 in LDS
+
+// Raw buffer loads issued from inline asm, invisible to the compiler's waitcnt pass, with hand-counted waits (the
+// scheme of k_encode_fixed1d_np): vmcnt counts loads and stores together, in issue order.
+typedef int v1_v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v1_v4i v1_rsrc(const void* p, uint32_t bytes)
 {
-  __shared__ uint32_t red[V1T / 64];
-  const uint32_t tid = threadIdx.x, t = blockIdx.x;
-  const bool wide_ok = F.vec && (((uintptr_t)F.data) & 15u) == 0;
-  V1Raw<DT> raw;
-  raw.load(F, t, wide_ok);
-  const uint64_t bl = (uint64_t)t * V1TILE + (uint64_t)tid * V1U;
-  uint32_t packed = 0, lsum = 0;
+  const uint64_t a = (uint64_t)p;
+  v1_v4i r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)((uint32_t)(a >> 32) & 0xffffu);  // stride 0
+  r.z = (int)bytes;                             // num_records: range check in bytes
+  r.w = 0x00020000;                             // raw buffer, no swizzle
+  return r;
+}
+
+typedef unsigned v1_u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v1_u4 v1_ld16(uint32_t off, v1_v4i rs)
+{
+  v1_u4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+  return v;
+}
+
+// wait until at most N vector memory operations are outstanding; ties the tile's raw words to after the wait
+template <int N, int NL>
+__device__ __forceinline__ void v1_wait_n(v1_u4 (&w)[NL])
+{
+  if constexpr (NL == 2)
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(w[0]), "+v"(w[1]) : "n"(N) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : "n"(N) : "memory");
+}
+
+// One tile's block lengths (bytes packed per lane) and the lane's sum.
+template <int DT>
+__device__ __forceinline__ uint32_t v1_count_tile(const FieldDesc& F, const Params& p, const V1Raw<DT>& raw,
+                                                  uint32_t t, uint32_t& lsum)
+{
+  const uint64_t bl = (uint64_t)t * V1TILE + (uint64_t)threadIdx.x * V1U;
+  const int cexp = -122 - p.minexp, maxprec = (int)min(p.maxprec, 64u);
+  uint32_t pk = 0;
+  lsum = 0;
 #pragma unroll
   for (uint32_t k = 0; k < V1U; k++) {
     float f[4];
     raw.block(k, f);
     uint32_t u[4], hdr, K;
     bool inf;
-    uint32_t len = v1_prep(f, -122 - p.minexp, (int)min(p.maxprec, 64u), u, hdr, K, inf);
+    uint32_t len;
+    if constexpr ((V1_ABLATE & 32) != 0) {  // measurement builds: no length computation in the count
+      len = 9u + ((__float_as_uint(f[0]) ^ __float_as_uint(f[3])) & 63u);
+      inf = false;
+    } else {
+      len = v1_prep(f, cexp, maxprec, u, hdr, K, inf);
+    }
     const bool valid = bl + k < F.nblocks;
     if (inf && valid) len = count_block<1>(f, p);
     len = valid ? len : 0u;  // <= 140
-    packed |= len << (8 * k);
+    pk |= len << (8 * k);
     lsum += len;
   }
-  lens8[(size_t)t * V1T + tid] = packed;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
-  if ((tid & 63u) == 0) red[tid >> 6] = lsum;
-  __syncthreads();
-  if (tid == 0) {
-    uint64_t tot = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < V1T / 64; w++) tot += red[w];
-    sums[t] = tot;
-  }
+  return pk;
 }
 
 template <int DT>
-__global__ __launch_bounds__(V1T) void k_encode1d_var_tile(FieldDesc F, Params p, const uint64_t* __restrict__ rbase,
-                                                           const uint32_t* __restrict__ lens8,
-                                                           uint32_t* __restrict__ out32, uint64_t* __restrict__ index,
-                                                           uint32_t index_shift, uint32_t ntiles)
+__global__ __launch_bounds__(V1T) void k_count1d_var_tile(FieldDesc F, Params p, uint32_t ntiles,
+                                                          uint64_t* __restrict__ sums, uint32_t* __restrict__ lens8,
+                                                          uint32_t* __restrict__ nover)
 {
-  __shared__ uint32_t tab[1280];  // pair table (lean-5 entries, rows n >= 3 empty)
-  __shared__ uint32_t rs[1024];   // window spread tables
-  __shared__ uint64_t win[V1Q];   // the tile's code from bit (base & 31) of its first stream word
-  __shared__ uint32_t scan_sh[V1T / 64];
-  __shared__ uint32_t s_special;
-  uint32_t* win32 = (uint32_t*)win;
-  const uint32_t tid = threadIdx.x, t = blockIdx.x;
-  for (uint32_t i = tid; i < 1280; i += V1T) tab[i] = g_plane_tab_var.v[i];
-  for (uint32_t i = tid; i < 1024; i += V1T) rs[i] = rspread_entry(i);
-  if (tid == 0) s_special = 0;
+  // V1CT consecutive tiles per workgroup. Full contiguous tiles are software-pipelined: tile i + 1's raw buffer loads
+  // are issued before tile i is counted (hand-counted waits), and nothing is stored until the loop is done -- the
+  // workgroups of a one-shot grid otherwise run in lock step, all loading and then all computing.
+  __shared__ uint32_t red[V1CT][V1T / 64];
+  const uint32_t tid = threadIdx.x, t0 = blockIdx.x * V1CT;
+  if (blockIdx.x == 0 && tid == 0) *nover = 0u;  // the oversized-tile list of k_encode1d_var_tile starts empty
   const bool wide_ok = F.vec && (((uintptr_t)F.data) & 15u) == 0;
-  V1Raw<DT> raw;
-  raw.load(F, t, wide_ok);
-  const uint32_t lw = lens8[(size_t)t * V1T + tid];
-  const uint64_t B = rbase[t];
-  const uint32_t lb = (uint32_t)(B & 31u);
+  constexpr int NL = V1Raw<DT>::N;                                 // 16-byte loads per lane per tile
+  constexpr uint32_t TB = V1TILE * (DT == DT_BF16 ? 8u : 16u);     // bytes per tile
+  uint32_t packed[V1CT];
+  if (wide_ok && (uint64_t)(t0 + V1CT) * V1TILE <= F.n[0] / 4) {
+    const v1_v4i rs = v1_rsrc((const char*)F.data + (size_t)t0 * TB, V1CT * TB);
+    v1_u4 buf[2][NL];
+#pragma unroll
+    for (int h = 0; h < NL; h++) buf[0][h] = v1_ld16((tid * NL + h) * 16u, rs);
+#pragma unroll
+    for (uint32_t i = 0; i < V1CT; i++) {
+      if (i + 1 < V1CT) {
+#pragma unroll
+        for (int h = 0; h < NL; h++) buf[(i + 1) & 1][h] = v1_ld16((i + 1) * TB + (tid * NL + h) * 16u, rs);
+        v1_wait_n<NL>(buf[i & 1]);
+      } else {
+        v1_wait_n<0>(buf[i & 1]);
+      }
+      V1Raw<DT> cur;
+#pragma unroll
+      for (int h = 0; h < NL; h++) {
+        const v1_u4 v = buf[i & 1][h];
+        cur.w[h] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      uint32_t lsum;
+      packed[i] = v1_count_tile<DT>(F, p, cur, t0 + i, lsum);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
+      if ((tid & 63u) == 0) red[i][tid >> 6] = lsum;
+    }
+  } else {  // partial tiles, the padded last block, strided or unaligned input
+#pragma unroll
+    for (uint32_t i = 0; i < V1CT; i++) {
+      uint32_t lsum = 0;
+      packed[i] = 0;
+      if (t0 + i < ntiles) {
+        V1Raw<DT> raw;
+        raw.load(F, t0 + i, wide_ok);
+        packed[i] = v1_count_tile<DT>(F, p, raw, t0 + i, lsum);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
+      if ((tid & 63u) == 0) red[i][tid >> 6] = lsum;
+    }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < V1CT; i++)
+    if (t0 + i < ntiles) lens8[(size_t)(t0 + i) * V1T + tid] = packed[i];
+  __syncthreads();
+  if (tid < V1CT && t0 + tid < ntiles) {
+    uint64_t tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < V1T / 64; w++) tot += red[tid][w];
+    sums[t0 + tid] = tot;
+  }
+}
+
+// One tile (raw words and the lane's byte lengths lw given) coded into the window `win`, from bit B & 127 (the
+// 16-byte stream boundary below the tile's first bit); tab / rs already in LDS. Ends with the window complete
+// (barrier) and the block index written.
+template <int DT>
+__device__ __forceinline__ void v1_tile_code(const FieldDesc& F, const Params& p, uint32_t t, uint64_t B,
+                                             const V1Raw<DT>& raw, uint32_t lw, uint64_t* __restrict__ index,
+                                             uint32_t index_shift, const uint32_t* tab, const uint32_t* rs,
+                                             uint64_t* win, uint32_t* scan_sh, uint32_t* s_special)
+{
+  uint32_t* win32 = (uint32_t*)win;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lb = (uint32_t)(B & 127u);
   uint32_t len[V1U], lsum = 0;
 #pragma unroll
   for (uint32_t k = 0; k < V1U; k++) {
     len[k] = (lw >> (8 * k)) & 255u;
     lsum += len[k];
   }
-  uint32_t total;
-  const uint32_t excl = lb + block_exclusive_scan<V1T>(lsum, &total, scan_sh);
-  if (lsum) {  // the two words this lane shares with its neighbours start at zero (lane 0: the bits below lb too)
+  uint32_t tot_unused;
+  const uint32_t excl = lb + block_exclusive_scan<V1T>(lsum, &tot_unused, scan_sh);
+  if (lsum) {  // the two words this lane shares with its neighbours start at zero
     win[excl >> 6] = 0ull;
     win[(excl + lsum - 1) >> 6] = 0ull;
   }
+  if (tid == 0) *s_special = 0;
   __syncthreads();
 
   // ---- prepare and code the lane's blocks one at a time: a 64-bit accumulator; whole words are plain LDS stores,
@@ -633,10 +719,23 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_tile(FieldDesc F, Params p
     raw.block(k, f);
     uint32_t u[4], hdr, K;
     bool inf;
-    (void)v1_prep(f, cexp, maxprec, u, hdr, K, inf);  // the length comes from the count pass
+    if constexpr ((V1_ABLATE & 16) != 0) {
+      for (int i = 0; i < 4; i++) u[i] = __float_as_uint(f[i]);
+      hdr = 3u + (u[0] >> 23);
+      K = 16;
+      inf = false;
+    } else {
+      (void)v1_prep(f, cexp, maxprec, u, hdr, K, inf);  // the length comes from the count pass
+    }
     bool sp = inf && bl + k < F.nblocks;
     uint64_t c0, c1;
-    v1_code(u, hdr, len[k], K, tab, rs, c0, c1, sp);
+    if constexpr ((V1_ABLATE & 2) != 0) {  // measurement builds: no coder (the prepared words stand in for the code)
+      c0 = ((uint64_t)u[1] << 32 | u[0]) ^ hdr;
+      c1 = (uint64_t)u[3] << 32 | u[2];
+      sp = false;
+    } else {
+      v1_code(u, hdr, len[k], K, tab, rs, c0, c1, sp);
+    }
     sp = sp && len[k];
     if (sp) c0 = c1 = 0ull;  // coded below by the generic coder, OR-ed into these zero bits
     spmask |= (uint32_t)sp << k;
@@ -664,9 +763,9 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_tile(FieldDesc F, Params p
     acc &= (1ull << fill) - 1ull;
   }
   if (fill) atomicOr((unsigned long long*)&win[q], (unsigned long long)acc);
-  if (spmask) s_special = 1u;
+  if (spmask) *s_special = 1u;
   __syncthreads();
-  if (s_special) {  // Inf / NaN blocks, long group phases, codes past 128 bits: the generic coder
+  if (*s_special) {  // Inf / NaN blocks, long group phases, codes past 128 bits: the generic coder
     uint32_t o = excl;
 #pragma unroll
     for (uint32_t k = 0; k < V1U; k++) {
@@ -685,20 +784,50 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_tile(FieldDesc F, Params p
 #pragma unroll
     for (uint32_t k = 0; k < V1U; k++) {
       const uint64_t b = bl + k;
-      if (len[k] && (b & ((1ull << index_shift) - 1ull)) == 0) index[b >> index_shift] = B - lb + o;
+      if (len[k] && (b & ((1ull << index_shift) - 1ull)) == 0) index[b >> index_shift] = (B & ~127ull) + o;
       o += len[k];
     }
   }
 
-  // ---- store the window: whole 32-bit stream words from word B >> 5, coalesced
-  const uint64_t g0 = B >> 5;
-  const uint32_t nw = (lb + total + 31u) >> 5;
+}
+
+// The window's 16-byte chunks c (stream words 4c .. 4c + 3 from word g0 = (B >> 7) * 4): the tile owns words kf .. kl;
+// the first / last chunk holds words of the neighbouring tiles and the two words it shares with them (atomicOr), so
+// those two chunks go word by word.
+__device__ __forceinline__ void v1_edge_chunk(uint32_t c, const uint32_t* win32, uint32_t* __restrict__ out32,
+                                              uint64_t g0, uint32_t kf, uint32_t kl, bool head_shared,
+                                              bool tail_shared)
+{
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t k = 4u * c + j;
+    if (k < kf || k > kl) continue;
+    const uint32_t val = win32[k];
+    if ((k == kf && head_shared) || (k == kl && tail_shared)) atomicOr(out32 + g0 + k, val);
+    else out32[g0 + k] = val;
+  }
+}
+
+// Store the coded window of tile t (total bits from B): every interior chunk is one ds_read_b128 + one 16-byte store.
+__device__ __forceinline__ void v1_tile_store(uint32_t t, uint64_t B, uint32_t total, const uint64_t* win,
+                                              uint32_t* __restrict__ out32, uint32_t ntiles)
+{
+  const uint32_t* win32 = (const uint32_t*)win;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lb = (uint32_t)(B & 127u);
+  // ---- store the window: 16-byte chunks of stream words from word g0 = (B >> 7) * 4, coalesced. The tile owns
+  // words kf .. kl; the first / last chunk holds words of the neighbouring tiles and the two words it shares with
+  // them (atomicOr), so those two chunks go word by word, every other chunk is one ds_read_b128 + one 16-byte store.
+  const uint64_t g0 = (B >> 7) << 2;
+  const uint32_t kf = lb >> 5, kl = (lb + total - 1u) >> 5;
+  const bool head_shared = (lb & 31u) != 0;
   const bool last_tile = t == ntiles - 1;
   const bool tail_shared = ((lb + total) & 31u) != 0 && !last_tile;
-  for (uint32_t k = tid; k < nw; k += V1T) {
-    const uint32_t val = win32[k];
-    if ((k == 0 && lb != 0) || (k == nw - 1 && tail_shared)) atomicOr(out32 + g0 + k, val);
-    else out32[g0 + k] = val;
+  const uint32_t nch = (V1_ABLATE & 4) ? 0u : (kl >> 2) + 1u;
+  const bool wide = (((uintptr_t)out32) & 15u) == 0;
+  for (uint32_t c = tid; c < nch; c += V1T) {
+    if (wide && c != 0 && c != nch - 1) *(uint4*)(out32 + g0 + 4u * c) = *(const uint4*)(win32 + 4u * c);
+    else v1_edge_chunk(c, win32, out32, g0, kf, kl, head_shared, tail_shared);
   }
   if (last_tile && tid == 0) {
     const uint64_t endw = (B + total + 31) >> 5;
@@ -706,11 +835,87 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_tile(FieldDesc F, Params p
   }
 }
 
-// The tile form's workspace: sums[ntiles], base[ntiles + 1] (uint64), then the byte lengths of whole tiles.
+// Load, code and store one tile.
+template <int DT>
+__device__ __forceinline__ void v1_tile(const FieldDesc& F, const Params& p, uint32_t t, uint64_t B, uint32_t total,
+                                        const uint32_t* __restrict__ lens8, uint32_t* __restrict__ out32,
+                                        uint64_t* __restrict__ index, uint32_t index_shift, uint32_t ntiles,
+                                        const uint32_t* tab, const uint32_t* rs, uint64_t* win, uint32_t* scan_sh,
+                                        uint32_t* s_special)
+{
+  const bool wide_ok = F.vec && (((uintptr_t)F.data) & 15u) == 0;
+  V1Raw<DT> raw;
+  raw.load(F, t, wide_ok);
+  const uint32_t lw = lens8[(size_t)t * V1T + threadIdx.x];
+  v1_tile_code<DT>(F, p, t, B, raw, lw, index, index_shift, tab, rs, win, scan_sh, s_special);
+  v1_tile_store(t, B, total, win, out32, ntiles);
+}
+
+// qwords of window a tile needs: its bits from bit B & 127 of the window (the 16-byte stream boundary below B), plus
+// the two qwords the accumulator may touch past its last bit (a special block's zero third word)
+__device__ __forceinline__ uint32_t v1_tile_qwords(uint64_t B, uint32_t total)
+{
+  return ((uint32_t)(B & 127u) + total + 63u) / 64u + 2u;
+}
+
+template <int DT>
+__global__ __launch_bounds__(V1T) void k_encode1d_var_tile(FieldDesc F, Params p, const uint64_t* __restrict__ rbase,
+                                                           const uint32_t* __restrict__ lens8,
+                                                           uint32_t* __restrict__ out32, uint64_t* __restrict__ index,
+                                                           uint32_t index_shift, uint32_t ntiles,
+                                                           uint32_t* __restrict__ over)
+{
+  __shared__ uint32_t tab[V1TAB];  // pair table rows 0..3 (lean-5 entries, row 3 empty)
+  __shared__ uint32_t rs[1024];    // window spread tables
+  __shared__ __attribute__((aligned(16))) uint64_t win[V1QS];  // the tile's code from bit base & 127 of its window
+  __shared__ uint32_t scan_sh[V1T / 64];
+  __shared__ uint32_t s_special;
+  const uint32_t t = blockIdx.x;
+  const uint64_t B = rbase[t];
+  const uint32_t total = (uint32_t)(rbase[t + 1] - B);
+  if (v1_tile_qwords(B, total) > V1QS) {  // oversized: listed for k_encode1d_var_tile_big (over[0] = count)
+    if (threadIdx.x == 0) over[1 + atomicAdd(over, 1u)] = t;
+    return;
+  }
+  for (uint32_t i = threadIdx.x; i < V1TAB; i += V1T) tab[i] = g_plane_tab_var.v[i];
+  for (uint32_t i = threadIdx.x; i < 1024; i += V1T) rs[i] = rspread_entry(i);
+  v1_tile<DT>(F, p, t, B, total, lens8, out32, index, index_shift, ntiles, tab, rs, win, scan_sh, &s_special);
+}
+
+template <int DT>
+__global__ __launch_bounds__(V1T) void k_encode1d_var_tile_big(FieldDesc F, Params p,
+                                                               const uint64_t* __restrict__ rbase,
+                                                               const uint32_t* __restrict__ lens8,
+                                                               uint32_t* __restrict__ out32,
+                                                               uint64_t* __restrict__ index, uint32_t index_shift,
+                                                               uint32_t ntiles, const uint32_t* __restrict__ over)
+{
+  __shared__ uint32_t tab[V1TAB];
+  __shared__ uint32_t rs[1024];
+  __shared__ __attribute__((aligned(16))) uint64_t win[V1Q + 2];
+  __shared__ uint32_t scan_sh[V1T / 64];
+  __shared__ uint32_t s_special;
+  const uint32_t n = over[0];
+  if (blockIdx.x >= n) return;
+  for (uint32_t i = threadIdx.x; i < V1TAB; i += V1T) tab[i] = g_plane_tab_var.v[i];
+  for (uint32_t i = threadIdx.x; i < 1024; i += V1T) rs[i] = rspread_entry(i);
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t t = over[1 + i];
+    const uint64_t B = rbase[t];
+    const uint32_t total = (uint32_t)(rbase[t + 1] - B);
+    v1_tile<DT>(F, p, t, B, total, lens8, out32, index, index_shift, ntiles, tab, rs, win, scan_sh, &s_special);
+    __syncthreads();  // the window and scan slots are reused by the next tile
+  }
+}
+
+// The tile form's workspace: sums[ntiles], base[ntiles + 1] (uint64), the oversized-tile list (count + ntiles
+// uint32, rounded to 8 bytes), then the byte lengths of whole tiles.
+static inline uint64_t v1_list_words(uint64_t ntiles) { return (ntiles + 2) / 2; }  // uint64 words
+
 size_t var1d_tile_workspace_bytes(uint64_t nblocks)
 {
   const uint64_t ntiles = (nblocks + V1TILE - 1) / V1TILE;
-  return (size_t)((2 * ntiles + 2) * 8 + ntiles * V1TILE);
+  return (size_t)((2 * ntiles + 2 + v1_list_words(ntiles)) * 8 + ntiles * V1TILE);
 }
 
 hipError_t launch_encode1d_var_tile(const FieldDesc& F, const Params& p, uint32_t* out32, uint64_t* ws,
@@ -721,17 +926,24 @@ hipError_t launch_encode1d_var_tile(const FieldDesc& F, const Params& p, uint32_
   const uint32_t ntiles = (uint32_t)((F.nblocks + V1TILE - 1) / V1TILE);
   uint64_t* sums = ws;
   uint64_t* base = ws + ntiles;
-  uint32_t* lens8 = (uint32_t*)(ws + 2 * (size_t)ntiles + 2);
-  if (F.dtype == DT_BF16) k_count1d_var_tile<DT_BF16><<<ntiles, V1T, 0, st>>>(F, p, sums, lens8);
-  else k_count1d_var_tile<DT_F32><<<ntiles, V1T, 0, st>>>(F, p, sums, lens8);
+  uint32_t* over = (uint32_t*)(ws + 2 * (size_t)ntiles + 2);
+  uint32_t* lens8 = (uint32_t*)(ws + 2 * (size_t)ntiles + 2 + v1_list_words(ntiles));
+  const uint32_t ncw = (ntiles + V1CT - 1) / V1CT;
+  if (F.dtype == DT_BF16) k_count1d_var_tile<DT_BF16><<<ncw, V1T, 0, st>>>(F, p, ntiles, sums, lens8, over);
+  else k_count1d_var_tile<DT_F32><<<ncw, V1T, 0, st>>>(F, p, ntiles, sums, lens8, over);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = launch_scan_ranges(sums, ntiles, base, d_total, out32, d_base, st);
   if (e != hipSuccess) return e;
-  if (F.dtype == DT_BF16)
-    k_encode1d_var_tile<DT_BF16><<<ntiles, V1T, 0, st>>>(F, p, base, lens8, out32, index, index_shift, ntiles);
-  else
-    k_encode1d_var_tile<DT_F32><<<ntiles, V1T, 0, st>>>(F, p, base, lens8, out32, index, index_shift, ntiles);
+  const uint32_t nbig = std::min(ntiles, 1280u);  // grid-stride workgroups of the oversized-tile pass (5 per CU)
+  if (F.dtype == DT_BF16) {
+    k_encode1d_var_tile<DT_BF16><<<ntiles, V1T, 0, st>>>(F, p, base, lens8, out32, index, index_shift, ntiles, over);
+    k_encode1d_var_tile_big<DT_BF16><<<nbig, V1T, 0, st>>>(F, p, base, lens8, out32, index, index_shift, ntiles,
+                                                           over);
+  } else {
+    k_encode1d_var_tile<DT_F32><<<ntiles, V1T, 0, st>>>(F, p, base, lens8, out32, index, index_shift, ntiles, over);
+    k_encode1d_var_tile_big<DT_F32><<<nbig, V1T, 0, st>>>(F, p, base, lens8, out32, index, index_shift, ntiles, over);
+  }
   return hipGetLastError();
 }
 

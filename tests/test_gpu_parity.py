@@ -706,8 +706,8 @@ def test_var1d_closed_form_coder(gc, orc, mode):
 @pytest.mark.parametrize("env", ["spin0", "single_pass", "range"])
 @pytest.mark.parametrize("mode", ["acc1e-6", "acc1e-3", "prec32", "expert_max", "bf16_acc1e-6"])
 def test_var1d_encoder_forms(gc, orc, env, mode, monkeypatch):
-    """The 1-D variable-rate encoder's other forms (the default is a count per 1024-block tile + scan + the tile
-    coder placed by the scan), bit-exact vs the oracle: `single_pass` places the tiles by a decoupled look-back
+    """The 1-D variable-rate encoder's other forms (the default is a count per 1024-block tile + scan + the tile coder
+    placed by the scan), bit-exact vs the oracle: `single_pass` places the tiles by a decoupled look-back
     (GCOW_VAR1D_SINGLE_PASS), `spin0` also makes every tile compute a not-yet-published predecessor's total itself
     (its no-dispatch-order fallback), `range` is count + scan + k_encode1d_var over larger ranges (GCOW_VAR1D_FORM)."""
     if env == "range":
@@ -728,6 +728,44 @@ def test_var1d_encoder_forms(gc, orc, env, mode, monkeypatch):
     d = gc.decode(e)
     torch.cuda.synchronize()
     assert np.array_equal(d.cpu().numpy().view(np.uint32), orc.decompress(w_ref, a.shape, op).view(np.uint32))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("appended", [False, True])
+def test_var1d_mixed_tile_sizes(gc, orc, dtype, appended):
+    """The default 1-D variable-rate form codes tiles of up to 95 bits per block in a small LDS window
+    (k_encode1d_var_tile) and larger ones in a second pass (k_encode1d_var_tile_big). Tiles (4096 values) alternate
+    between N(0, 1) (about 110 bits per block at accuracy 1e-6) and N(0, 1e-3) (about 60), with Inf / NaN blocks in
+    both kinds and a ragged tail, so both kernels write words their neighbours share. `appended`: the stream starts
+    at a device bit offset (gcow_encode_device_append through a chunked encode)."""
+    rng = np.random.default_rng(97)
+    n = 4096 * 21 + 4 * 333 + 3
+    a = rng.standard_normal(n).astype(np.float32)
+    for t in range(0, n, 4096):
+        if (t // 4096) % 3 != 1:
+            a[t:t + 4096] *= np.float32(1e-3)
+    a[4096 * 4 + 17] = np.inf
+    a[4096 * 7 + 401] = np.nan
+    if dtype == "bf16":
+        a = (a.view(np.uint32) >> 16).astype(np.uint16)
+    op = orc.accuracy(1e-6)
+    if not appended:
+        _check_vs_oracle(gc, orc, a, op, index_stride=16)
+        return
+    w_ref, bits_ref = orc.compress(a, op)
+    x = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    if dtype == "bf16":
+        x = x.view(torch.bfloat16)
+    params = P(gc, op)
+    words = torch.zeros(gc.max_output_bytes(x.shape, params, x.dtype) // 8 + 4, dtype=torch.int64, device="cuda")
+    cuts = [0, 4096 * 9 + 4 * 77, n]  # block-aligned: the second chunk starts mid-word
+    bits = torch.zeros(len(cuts), dtype=torch.int64, device="cuda")
+    for i in range(len(cuts) - 1):
+        gc.encode_append(x[cuts[i]:cuts[i + 1]], params, words, bits[i:i + 1], bits[i + 1:i + 2])
+    torch.cuda.synchronize()
+    assert int(bits[-1]) == bits_ref
+    nw = (bits_ref + 63) // 64
+    assert np.array_equal(words[:nw].cpu().numpy().view(np.uint64), w_ref.view(np.uint64)[:nw])
 
 
 def test_c5_full_size_bf16_accuracy(gc, orc):

@@ -37,6 +37,26 @@ def length_formula(u, prec):
     return n + (B - 2 if c == B else c)
 
 
+def length_b4_integer(u, prec):
+    """The 4-coefficient form var1d.hip's v1_prep evaluates without compare-to-mask selects:
+    4 + 4 K - sum_{j<3} c_j + sum_{j<3} e_j with c_j = min(z_j, K + 1) and e_j = [c_j <= K] * bit 31 of u_j << c_j
+    (the hardware shift takes the count's low 5 bits)."""
+    kmin = 32 - prec if prec < 32 else 0
+    K = 31 - kmin
+
+    def ffbh(v):
+        return 0xFFFFFFFF if v == 0 else 32 - int(v).bit_length()
+
+    S2 = int(u[2]) | int(u[3])
+    S1 = int(u[1]) | S2
+    S0 = int(u[0]) | S1
+    n = 4 + 4 * K
+    for uj, S in ((int(u[0]), S0), (int(u[1]), S1), (int(u[2]), S2)):
+        c = min(ffbh(S), K + 1)
+        n += ((((uj << (c & 31)) & 0xFFFFFFFF) >> 31) & min(K + 1 - c, 1)) - c
+    return n
+
+
 def length_leading_planes(u, prec):
     """The earlier form of the same pass (leading planes L_j and their suffix maxima R_j), kept as a cross-check."""
     B = len(u)
@@ -98,6 +118,8 @@ def test_length_formula_matches_coder(orc, size):
         assert length_formula(u, prec) == bits, (u.tolist(), prec)
         assert length_per_plane(u, prec) == bits, (u.tolist(), prec)
         assert length_leading_planes(u, prec) == bits, (u.tolist(), prec)
+        if size == 4:
+            assert length_b4_integer(u, prec) == bits, (u.tolist(), prec)
 
 
 def test_length_formula_extremes(orc):
@@ -110,3 +132,5 @@ def test_length_formula_extremes(orc):
                 words[:] = 0
                 _, _, bits = orc.encode_ints(u, 1 << 30, prec, words=words)
                 assert length_formula(u, prec) == bits
+                if size == 4:
+                    assert length_b4_integer(u, prec) == bits

@@ -5,11 +5,11 @@
 set -e
 cd "$(dirname "$0")/../.."
 make -s -C gcow_amd/csrc
-mkdir -p ab
+OUT=${ABL_DIR:-ab}; mkdir -p $OUT
 B=gcow_amd/csrc/build
 for a in "$@"; do  # NAME=-DFLAGS,... e.g. 8=-DV1_ABLATE=8 or poll1=-DV1_POLL=1
   name=${a%%=*}; flags=${a#*=}; flags=${flags//,/ }
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Igcow_amd/csrc $flags \
-    -c gcow_amd/csrc/var1d.hip -o ab/var1d_$name.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab/v1ab_$name.so $B/gcow_kernels.o $B/gcow_blocks.o ab/var1d_$name.o $B/gcow_api.o
+    -c gcow_amd/csrc/var1d.hip -o $OUT/var1d_$name.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/v1ab_$name.so $B/gcow_kernels.o $B/gcow_blocks.o $OUT/var1d_$name.o $B/gcow_api.o
 done

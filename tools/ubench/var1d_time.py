@@ -8,7 +8,8 @@ import time
 
 import torch
 
-os.environ.setdefault("GCOW_VAR1D_SINGLE_PASS", "1")  # the single-pass form (the ablation builds' kernel)
+if "--sp" in sys.argv:
+    os.environ["GCOW_VAR1D_SINGLE_PASS"] = "1"  # the look-back form (else the default tile form)
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 if "--lib" in sys.argv:
@@ -46,12 +47,13 @@ for tol in (1e-6, 1e-3):
             enc(xb)
         torch.cuda.synchronize()
     d = {"cold_ms": round(cold, 4), "steady_ms": round(timed(lambda: enc(xb), 0, 100), 4)}
-    os.environ["GCOW_VAR1D_STATS"] = "1"  # look-back polls / fallbacks / windows of one launch
-    enc(xb)
-    torch.cuda.synchronize()
-    os.environ.pop("GCOW_VAR1D_STATS")
-    nt = (n // 4 + 1023) // 1024
-    d["lookback_polls_fallbacks_windows"] = enc.ws[2 * nt:2 * nt + 3].tolist()
+    if "--sp" in sys.argv:
+        os.environ["GCOW_VAR1D_STATS"] = "1"  # look-back polls / fallbacks / windows of one launch
+        enc(xb)
+        torch.cuda.synchronize()
+        os.environ.pop("GCOW_VAR1D_STATS")
+        nt = (n // 4 + 1023) // 1024
+        d["lookback_polls_fallbacks_windows"] = enc.ws[2 * nt:2 * nt + 3].tolist()
     out["acc%g" % tol] = d
     del enc
 print(json.dumps(out), flush=True)
