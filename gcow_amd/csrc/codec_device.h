@@ -251,6 +251,39 @@ __device__ __forceinline__ void transpose32_pinned(uint32_t* a)
   pin32(a);
 }
 
+// The four S < 16 stages on 16 words: after the S = 16 stage of transpose32, words 16..31 (planes 16..31) and words
+// 0..15 (planes 0..15) only mix among themselves (the stages commute), so a coder that stops above plane 16 never
+// needs the lower half's stages.
+template <int S, uint32_t M>
+__device__ __forceinline__ void transpose16_stage(uint32_t* a)
+{
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    if (i & S) continue;
+    const uint32_t t = ((a[i] >> S) ^ a[i + S]) & M;
+    a[i + S] ^= t;
+    a[i] ^= t << S;
+  }
+}
+
+__device__ __forceinline__ void pin16(uint32_t* a)
+{
+#pragma unroll
+  for (int i = 0; i < 16; i++) asm volatile("" : "+v"(a[i]));
+}
+
+__device__ __forceinline__ void transpose_half_pinned(uint32_t* a)
+{
+  transpose16_stage<8, 0x00FF00FFu>(a);
+  pin16(a);
+  transpose16_stage<4, 0x0F0F0F0Fu>(a);
+  pin16(a);
+  transpose16_stage<2, 0x33333333u>(a);
+  pin16(a);
+  transpose16_stage<1, 0x55555555u>(a);
+  pin16(a);
+}
+
 __device__ __forceinline__ void transpose32(uint32_t* a)
 {
   transpose32_stage<16, 0x0000FFFFu>(a);
@@ -548,14 +581,14 @@ __device__ __forceinline__ void encode_plane64_dup(W& w, uint64_t P, uint32_t& b
   }
 }
 
-template <int K, class W>
+template <int K, int KLO, class W>
 __device__ __forceinline__ void encode_planes64_dup(W& w, const uint32_t* t, int kstart, int kmin, uint32_t budget,
                                                     uint32_t& bits, uint32_t& n, const uint32_t* dup)
 {
-  if constexpr (K >= 0) {
+  if constexpr (K >= KLO) {
     if (K < kmin || bits >= budget) return;
     if (K <= kstart) encode_plane64_dup(w, (uint64_t)t[K] | ((uint64_t)t[32 + K] << 32), bits, n, dup);
-    encode_planes64_dup<K - 1>(w, t, kstart, kmin, budget, bits, n, dup);
+    encode_planes64_dup<K - 1, KLO>(w, t, kstart, kmin, budget, bits, n, dup);
   }
 }
 
@@ -574,14 +607,25 @@ __device__ __forceinline__ uint32_t encode_ints64_dup(W& w, uint32_t* u, uint32_
   asm volatile("" : "+v"(any));
   pin32(u);
   pin32(u + 32);
-  transpose32_pinned(u);
-  transpose32_pinned(u + 32);
+  // planes 16..31 first (the S = 16 stage, then the upper halves); the lower halves' stages only when some lane of
+  // the wave codes a plane below 16 (a fixed-rate budget usually runs out above it)
+  transpose32_stage<16, 0x0000FFFFu>(u);
+  pin32(u);
+  transpose32_stage<16, 0x0000FFFFu>(u + 32);
+  pin32(u + 32);
+  transpose_half_pinned(u + 16);
+  transpose_half_pinned(u + 48);
   const int top = any ? 31 - (int)__builtin_clz(any) : -1;  // highest plane with a one-bit
   const int kstart = max(top, kmin - 1);
   uint32_t bits = min((uint32_t)(31 - kstart), budget);
   w.skip(bits);
   uint32_t n = 0;
-  encode_planes64_dup<31>(w, u, kstart, kmin, budget, bits, n, dup);
+  encode_planes64_dup<31, 16>(w, u, kstart, kmin, budget, bits, n, dup);
+  if (__any(kmin <= 15 && bits < budget)) {
+    transpose_half_pinned(u);
+    transpose_half_pinned(u + 32);
+    encode_planes64_dup<15, 0>(w, u, kstart, kmin, budget, bits, n, dup);
+  }
   return bits < budget ? bits : budget;
 }
 
