@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """C2 (256 Mi fp32 1-D, fixed rate 16 and 8) encode: A/B of coder variants selected by an environment variable read
-at each launch (default GCOW_FIXED1D_LEAN: 6 = lean-6, 7 = lean-7), interleaved in one process over several rounds.
+at each launch (default GCOW_FIXED1D_LEAN: 6 = lean-6, 7 = the variant under test), interleaved in one process over
+several rounds in ABBA order with 2 s pauses (a variant run right after another's burst starts in a deeper DVFS dip).
 Per variant and round: the driver protocol (5 untimed + 20 timed launches, mean of the HIP-event times, the bench's
 `value`) and steady state (after 0.25 s of back-to-back launches, 100 launches). The variants' streams are compared
 with each other (the GPU parity tests compare them with the oracle). One JSON line per case.
@@ -58,9 +59,9 @@ def main():
         res = {"case": "c2_rate%d" % rate, "var": a.var}
         streams = {}
         for rnd in range(a.rounds):
-            for v in vals:
+            for v in (vals if rnd % 2 == 0 else vals[::-1]):  # ABBA: the DVFS state after a burst favours neither
                 os.environ[a.var] = v
-                time.sleep(0.5)  # let the clock settle between variants
+                time.sleep(2.0)  # let the clock settle between variants
                 cold, per = timed(lambda: enc(x), 5, 20)
                 st = steady(lambda: enc(x))
                 if rnd == 0:
