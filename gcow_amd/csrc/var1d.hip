@@ -579,8 +579,9 @@ __device__ __forceinline__ void v1_wait_n(v1_u4 (&w)[NL])
     asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : "n"(N) : "memory");
 }
 
-// One tile's block lengths (bytes packed per lane) and the lane's sum.
-template <int DT>
+// One tile's block lengths (bytes packed per lane) and the lane's sum. FULL: every block of the tile is inside the
+// field (no per-block range check).
+template <int DT, bool FULL = false>
 __device__ __forceinline__ uint32_t v1_count_tile(const FieldDesc& F, const Params& p, const V1Raw<DT>& raw,
                                                   uint32_t t, uint32_t& lsum)
 {
@@ -601,7 +602,7 @@ __device__ __forceinline__ uint32_t v1_count_tile(const FieldDesc& F, const Para
     } else {
       len = v1_prep(f, cexp, maxprec, u, hdr, K, inf);
     }
-    const bool valid = bl + k < F.nblocks;
+    const bool valid = FULL || bl + k < F.nblocks;
     if (inf && valid) len = count_block<1>(f, p);
     len = valid ? len : 0u;  // <= 140
     pk |= len << (8 * k);
@@ -646,7 +647,7 @@ __global__ __launch_bounds__(V1T) void k_count1d_var_tile(FieldDesc F, Params p,
         cur.w[h] = make_uint4(v.x, v.y, v.z, v.w);
       }
       uint32_t lsum;
-      packed[i] = v1_count_tile<DT>(F, p, cur, t0 + i, lsum);
+      packed[i] = v1_count_tile<DT, true>(F, p, cur, t0 + i, lsum);
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
       if ((tid & 63u) == 0) red[i][tid >> 6] = lsum;
