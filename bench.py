@@ -459,9 +459,14 @@ def leg_configs(ctx):
                             pin_memory=True)
         henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=8, device=ctx.dev)
         h_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 2, 5)
+        er = roof(n * 2, cbits / 8, k_ms,
+                  "k_count1d_var_tile + k_scan_ranges_mw + k_encode1d_var_tile (+ k_encode1d_var_tile_big)")
+        # HBM bytes of one encode (all four kernels) from a committed PMC pass (tools/c5_traffic.py); the input is read
+        # twice (count + coder) and the byte lengths written and read once
+        er["traffic"], src = load_pmc_traffic("k_count1d_var_tile", name + "_256Mi")
+        er["traffic_source"] = src
         out[name] = {"encode_ms": round(k_ms, 4), "encode_GiBps_input": round(gib(n * 2, k_ms), 2),
-                     "bits_per_value": round(cbits / n, 3),
-                     "encode_roofline": roof(n * 2, cbits / 8, k_ms, "k_count1d_var_tile + k_scan_ranges_mw + k_encode1d_var_tile (+ k_encode1d_var_tile_big)"),
+                     "bits_per_value": round(cbits / n, 3), "encode_roofline": er,
                      "host_path_ms": round(h_ms, 3), "host_path_GiBps_input": round(gib(n * 2, h_ms), 2),
                      "host_path_note": "pinned bf16 H2D + encode + D2H of the stream, 8 overlapped chunks (PCIe-bound)"}
         del enc, h_in, h_out, henc
