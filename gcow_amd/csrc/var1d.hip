@@ -329,6 +329,11 @@ __device__ uint64_t v1_lookback(uint64_t* status, uint32_t t, uint64_t base0, co
         atomicAdd((unsigned long long*)stats, (unsigned long long)polls);
         atomicAdd((unsigned long long*)stats + 1, (unsigned long long)fallbacks);
         atomicAdd((unsigned long long*)stats + 2, (unsigned long long)windows);
+        if (polls) {  // tiles that polled at all, the most polls of one tile, polls of the first 2048 tiles
+          atomicAdd((unsigned long long*)stats + 3, 1ull);
+          atomicMax((unsigned long long*)stats + 4, (unsigned long long)polls);
+          if (t < 2048) atomicAdd((unsigned long long*)stats + 5, (unsigned long long)polls);
+        }
       }
       return excl;
     }
@@ -506,14 +511,15 @@ hipError_t launch_encode1d_var_sp(const FieldDesc& F, const Params& p, uint32_t*
 {
   hipStream_t st = (hipStream_t)stream;
   const uint32_t ntiles = (uint32_t)((F.nblocks + V1TILE - 1) / V1TILE);
-  hipError_t e = hipMemsetAsync(ws, 0, (size_t)16 * ntiles + 32, st);
+  hipError_t e = hipMemsetAsync(ws, 0, (size_t)16 * ntiles + 64, st);
   if (e != hipSuccess) return e;
   uint64_t* status = ws;
   uint64_t* bnd = ws + ntiles;
   // GCOW_VAR1D_SPIN (tests): polls before a missing predecessor's total is computed locally; 0 exercises that path
   const char* ev = getenv("GCOW_VAR1D_SPIN");
   const uint32_t spin = ev ? (uint32_t)strtoul(ev, nullptr, 10) : V1SPIN;
-  // GCOW_VAR1D_STATS (measurement): polls, fallbacks and look-back windows summed into ws[2 ntiles .. + 3)
+  // GCOW_VAR1D_STATS (measurement): polls, fallbacks, look-back windows, polling tiles, most polls, polls of the
+  // first 2048 tiles into ws[2 ntiles .. + 6)
   uint64_t* stats = getenv("GCOW_VAR1D_STATS") ? ws + 2 * (size_t)ntiles : nullptr;
   if (F.dtype == DT_BF16)
     k_encode1d_var_sp<DT_BF16><<<ntiles, V1T, 0, st>>>(F, p, status, bnd, out32, index, index_shift, d_base, d_total,

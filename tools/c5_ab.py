@@ -74,8 +74,9 @@ def main():
                     torch.cuda.synchronize()
                     os.environ.pop("GCOW_VAR1D_STATS")
                     nt = (n // 4 + 1023) // 1024
-                    st_ = enc.ws[2 * nt:2 * nt + 3].tolist()
-                    res["lookback"] = {"tiles": nt, "polls": st_[0], "fallbacks": st_[1], "windows": st_[2]}
+                    st_ = enc.ws[2 * nt:2 * nt + 6].tolist()
+                    res["lookback"] = {"tiles": nt, "polls": st_[0], "fallbacks": st_[1], "windows": st_[2],
+                                       "polling_tiles": st_[3], "max_polls": st_[4], "polls_first_2048": st_[5]}
                 if rnd == 0:
                     streams[form] = (bits, e.stream().clone())
                 res.setdefault(form, []).append({"cold_ms": round(cold, 4), "first_ms": round(per[0], 4),
