@@ -53,7 +53,7 @@ for tol in (1e-6, 1e-3):
         torch.cuda.synchronize()
         os.environ.pop("GCOW_VAR1D_STATS")
         nt = (n // 4 + 1023) // 1024
-        d["lookback_polls_fallbacks_windows"] = enc.ws[2 * nt:2 * nt + 3].tolist()
+        d["lookback_polls_fallbacks_windows_polling_max_first2048"] = enc.ws[2 * nt:2 * nt + 6].tolist()
     out["acc%g" % tol] = d
     del enc
 print(json.dumps(out), flush=True)
