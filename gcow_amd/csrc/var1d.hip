@@ -42,7 +42,8 @@ constexpr uint32_t V1Q = (V1TILE * V1MAXB + 63) / 64 + 2;    // LDS window, 64-b
 constexpr uint64_t V1VAL = (1ull << 62) - 1;                 // status word: flag << 62 | value
 // V1_ABLATE (measurement builds only, tools/ubench/var1d_ablate.sh; 0 in the product): 1 = no look-back (tile t at
 // t * 64 Ki bits), 2 = no coding (zero codes / prepared words, lengths kept), 4 = no window store, 8 = no pair loop,
-// 16 = no prepare in the tile coder (raw words as coefficients), 32 = no length computation in the tile count
+// 16 = no prepare in the tile coder (raw words as coefficients), 32 = no length computation in the tile count,
+// 64 = no input / length loads in the tile coder (synthetic words, 58-bit blocks)
 #ifndef V1_ABLATE
 #define V1_ABLATE 0
 #endif
@@ -852,8 +853,18 @@ __device__ __forceinline__ void v1_tile(const FieldDesc& F, const Params& p, uin
 {
   const bool wide_ok = F.vec && (((uintptr_t)F.data) & 15u) == 0;
   V1Raw<DT> raw;
-  raw.load(F, t, wide_ok);
-  const uint32_t lw = lens8[(size_t)t * V1T + threadIdx.x];
+  uint32_t lw;
+  if constexpr ((V1_ABLATE & 64) != 0) {  // measurement builds: no input or length loads (words from the tile index)
+    const uint32_t h = (t * 2654435761u) ^ (threadIdx.x * 40503u);
+#pragma unroll
+    for (int i = 0; i < V1Raw<DT>::N; i++)  // normal values near 5e-4 (bf16 / fp32 halves: sign, exponent 0x74)
+      raw.w[i] = make_uint4((h & 0x807f807fu) | 0x3a003a00u, ((h * 3u) & 0x807f807fu) | 0x3a003a00u,
+                            ((h * 5u) & 0x807f807fu) | 0x3a003a00u, ((h * 7u) & 0x807f807fu) | 0x3a003a00u);
+    lw = 0x3a3a3a3au;
+  } else {
+    raw.load(F, t, wide_ok);
+    lw = lens8[(size_t)t * V1T + threadIdx.x];
+  }
   v1_tile_code<DT>(F, p, t, B, raw, lw, index, index_shift, tab, rs, win, scan_sh, s_special);
   v1_tile_store(t, B, total, win, out32, ntiles);
 }
