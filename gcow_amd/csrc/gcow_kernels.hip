@@ -1602,10 +1602,13 @@ __global__ void k_decode_tail1d(FieldDesc F, Params p, const uint64_t* __restric
 // 0.5 M loads at 32 Ki ranges), so no second launch, no partials buffer and no inter-workgroup protocol.
 constexpr uint32_t kScanMwMax = 1u << 16;
 
+// gsums (optional): totals of consecutive groups of 8 ranges (the 1-D tile count writes them), so the earlier totals
+// each workgroup sums are 1/8 as many.
 __global__ __launch_bounds__(256) void k_scan_ranges_mw(const uint64_t* __restrict__ sums, uint32_t nranges,
                                                         uint64_t* __restrict__ base, uint64_t* __restrict__ total,
                                                         uint32_t* __restrict__ out32,
-                                                        const uint64_t* __restrict__ d_base)
+                                                        const uint64_t* __restrict__ d_base,
+                                                        const uint64_t* __restrict__ gsums)
 {
   constexpr uint32_t T = 256, K = 4, C = T * K;
   __shared__ uint64_t v[C];
@@ -1618,16 +1621,18 @@ __global__ __launch_bounds__(256) void k_scan_ranges_mw(const uint64_t* __restri
     const uint32_t j = t + T * k;
     v[j] = j < n ? sums[c0 + j] : 0ull;
   }
-  uint64_t pre = 0;  // every earlier range total, 8 loads in flight per thread
+  uint64_t pre = 0;  // every earlier range total (or group total), 8 loads in flight per thread
+  const uint64_t* ps = gsums ? gsums : sums;
+  const uint32_t pn = gsums ? c0 / 8u : c0;
   uint32_t i = t;
-  for (; i + 7 * T < c0; i += 8 * T) {
+  for (; i + 7 * T < pn; i += 8 * T) {
     uint64_t a[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) a[k] = sums[i + k * T];
+    for (int k = 0; k < 8; k++) a[k] = ps[i + k * T];
 #pragma unroll
     for (int k = 0; k < 8; k++) pre += a[k];
   }
-  for (; i < c0; i += T) pre += sums[i];
+  for (; i < pn; i += T) pre += ps[i];
   __syncthreads();
   uint64_t loc[K], s = 0;
 #pragma unroll
@@ -1675,10 +1680,10 @@ __global__ __launch_bounds__(256) void k_scan_ranges_mw(const uint64_t* __restri
 }
 
 static void scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* base, uint64_t* total, uint32_t* out32,
-                        const uint64_t* d_base, hipStream_t st)
+                        const uint64_t* d_base, hipStream_t st, const uint64_t* gsums = nullptr)
 {
-  if (nranges > 4096 && nranges <= kScanMwMax)
-    k_scan_ranges_mw<<<(nranges + 1023) / 1024, 256, 0, st>>>(sums, nranges, base, total, out32, d_base);
+  if (nranges > 4096 && (nranges <= kScanMwMax || gsums))
+    k_scan_ranges_mw<<<(nranges + 1023) / 1024, 256, 0, st>>>(sums, nranges, base, total, out32, d_base, gsums);
   else
     k_scan_ranges<<<1, 1024, 0, st>>>(sums, nranges, base, total, out32, d_base);
 }
@@ -2243,9 +2248,9 @@ hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint
 }
 
 hipError_t launch_scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* base, uint64_t* total, uint32_t* out32,
-                              const uint64_t* d_base, void* stream)
+                              const uint64_t* d_base, void* stream, const uint64_t* gsums)
 {
-  scan_ranges(sums, nranges, base, total, out32, d_base, S(stream));
+  scan_ranges(sums, nranges, base, total, out32, d_base, S(stream), gsums);
   return hipGetLastError();
 }
 

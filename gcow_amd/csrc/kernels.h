@@ -64,8 +64,9 @@ hipError_t launch_scan_blocks(const uint32_t* lens, uint32_t nblocks, uint64_t* 
 hipError_t launch_encode_tiles23(const FieldDesc& F, const Params& p, const TilePlan& plan, uint32_t* out32,
                                  uint64_t* ws_sums, uint64_t* ws_base, uint64_t* d_total, uint64_t* index,
                                  uint32_t index_shift, const uint64_t* d_base, void* stream);
+// gsums (optional): totals of consecutive groups of 8 ranges, which the many-workgroup scan sums instead of the ranges
 hipError_t launch_scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* base, uint64_t* total, uint32_t* out32,
-                              const uint64_t* d_base, void* stream);
+                              const uint64_t* d_base, void* stream, const uint64_t* gsums = nullptr);
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
 // Single-pass 1-D variable-rate encoder (var1d.hip): minbits <= 1, maxbits >= 160; ws = var1d_sp_workspace_bytes().
 size_t var1d_sp_workspace_bytes(uint64_t nblocks);

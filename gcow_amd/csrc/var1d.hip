@@ -621,8 +621,9 @@ __device__ __forceinline__ uint32_t v1_count_tile(const FieldDesc& F, const Para
 template <int DT>
 __global__ __launch_bounds__(V1T) void k_count1d_var_tile(FieldDesc F, Params p, uint32_t ntiles,
                                                           uint64_t* __restrict__ sums, uint32_t* __restrict__ lens8,
-                                                          uint32_t* __restrict__ nover)
+                                                          uint32_t* __restrict__ nover, uint64_t* __restrict__ gsums)
 {
+  static_assert(V1CT == 8, "the scan's group totals (gsums) cover 8 tiles");
   // V1CT consecutive tiles per workgroup. Full contiguous tiles are software-pipelined: tile i + 1's raw buffer loads
   // are issued before tile i is counted (hand-counted waits), and nothing is stored until the loop is done -- the
   // workgroups of a one-shot grid otherwise run in lock step, all loading and then all computing.
@@ -678,11 +679,19 @@ __global__ __launch_bounds__(V1T) void k_count1d_var_tile(FieldDesc F, Params p,
   for (uint32_t i = 0; i < V1CT; i++)
     if (t0 + i < ntiles) lens8[(size_t)(t0 + i) * V1T + tid] = packed[i];
   __syncthreads();
-  if (tid < V1CT && t0 + tid < ntiles) {
+  if (tid < 64) {  // wave 0: the tile totals, and their sum for the scan's group totals
     uint64_t tot = 0;
+    if (tid < V1CT && t0 + tid < ntiles) {
 #pragma unroll
-    for (uint32_t w = 0; w < V1T / 64; w++) tot += red[tid][w];
-    sums[t0 + tid] = tot;
+      for (uint32_t w = 0; w < V1T / 64; w++) tot += red[tid][w];
+      sums[t0 + tid] = tot;
+    }
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) {
+      const uint32_t lo = __shfl_xor((uint32_t)tot, o, 64), hi = __shfl_xor((uint32_t)(tot >> 32), o, 64);
+      tot += (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    if (tid == 0) gsums[blockIdx.x] = tot;
   }
 }
 
@@ -927,13 +936,13 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_tile_big(FieldDesc F, Para
 }
 
 // The tile form's workspace: sums[ntiles], base[ntiles + 1] (uint64), the oversized-tile list (count + ntiles
-// uint32, rounded to 8 bytes), then the byte lengths of whole tiles.
+// uint32, rounded to 8 bytes), the byte lengths of whole tiles, then the totals of groups of 8 tiles.
 static inline uint64_t v1_list_words(uint64_t ntiles) { return (ntiles + 2) / 2; }  // uint64 words
 
 size_t var1d_tile_workspace_bytes(uint64_t nblocks)
 {
   const uint64_t ntiles = (nblocks + V1TILE - 1) / V1TILE;
-  return (size_t)((2 * ntiles + 2 + v1_list_words(ntiles)) * 8 + ntiles * V1TILE);
+  return (size_t)((2 * ntiles + 2 + v1_list_words(ntiles) + (ntiles + V1CT - 1) / V1CT) * 8 + ntiles * V1TILE);
 }
 
 hipError_t launch_encode1d_var_tile(const FieldDesc& F, const Params& p, uint32_t* out32, uint64_t* ws,
@@ -946,12 +955,13 @@ hipError_t launch_encode1d_var_tile(const FieldDesc& F, const Params& p, uint32_
   uint64_t* base = ws + ntiles;
   uint32_t* over = (uint32_t*)(ws + 2 * (size_t)ntiles + 2);
   uint32_t* lens8 = (uint32_t*)(ws + 2 * (size_t)ntiles + 2 + v1_list_words(ntiles));
+  uint64_t* gsums = (uint64_t*)(lens8 + (size_t)ntiles * V1T);
   const uint32_t ncw = (ntiles + V1CT - 1) / V1CT;
-  if (F.dtype == DT_BF16) k_count1d_var_tile<DT_BF16><<<ncw, V1T, 0, st>>>(F, p, ntiles, sums, lens8, over);
-  else k_count1d_var_tile<DT_F32><<<ncw, V1T, 0, st>>>(F, p, ntiles, sums, lens8, over);
+  if (F.dtype == DT_BF16) k_count1d_var_tile<DT_BF16><<<ncw, V1T, 0, st>>>(F, p, ntiles, sums, lens8, over, gsums);
+  else k_count1d_var_tile<DT_F32><<<ncw, V1T, 0, st>>>(F, p, ntiles, sums, lens8, over, gsums);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = launch_scan_ranges(sums, ntiles, base, d_total, out32, d_base, st);
+  e = launch_scan_ranges(sums, ntiles, base, d_total, out32, d_base, st, gsums);
   if (e != hipSuccess) return e;
   const uint32_t nbig = std::min(ntiles, 1280u);  // grid-stride workgroups of the oversized-tile pass (5 per CU)
   if (F.dtype == DT_BF16) {
