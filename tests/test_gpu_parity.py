@@ -784,6 +784,24 @@ def test_c5_full_size_bf16_accuracy(gc, orc):
     assert np.array_equal(e.stream().cpu().numpy().view(np.uint64), w_ref)
 
 
+def test_var1d_more_than_64ki_tiles(gc, orc):
+    """Past 64 Ki tiles of 1024 blocks (256 Mi values) the range scan of the 1-D variable-rate encoder relies on the
+    count's 8-tile group totals (k_scan_ranges_mw with gsums); a ragged bucket just past that size, accuracy 1e-6 on
+    bf16, vs the threaded oracle."""
+    n = 256 * 1024 * 1024 + 3 * 4096 + 7
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    gc.fill_normal(x, 1e-3, seed=0x5EED, inject=True)
+    xb = x.to(torch.bfloat16)
+    del x
+    hb = xb.cpu().view(torch.int16).numpy().view(np.uint16)
+    op = orc.accuracy(1e-6)
+    w_ref, bits_ref = orc.compress(hb, op, threads=min(16, os.cpu_count() or 1))
+    e = gc.encode(xb, P(gc, op), index_stride=16)
+    torch.cuda.synchronize()
+    assert e.bits == bits_ref
+    assert np.array_equal(e.stream().cpu().numpy().view(np.uint64), w_ref)
+
+
 @pytest.mark.parametrize("nblocks", [1, 1023, 1024, 1025, 2048 + 5, 70001])
 @pytest.mark.parametrize("layout", ["contig", "offset1", "offset8", "stride2"])
 def test_var1d_bf16_load_paths(gc, orc, nblocks, layout):
