@@ -84,8 +84,10 @@ __device__ __forceinline__ uint32_t v1_prep(const float* f, int cexp, int maxpre
   inf = m > 0x7f7fffffu || __builtin_isunordered(f[0], f[1]) || __builtin_isunordered(f[2], f[3]);
   const uint32_t E = m >> 23;
   // get_precision, d = 1 (common.c:226-229); subnormal maxima clamp emax to -126 (encode.c:142-152)
-  const int prec = min(max((int)E + cexp, 0), maxprec);
-  K = (uint32_t)min(max(prec - 1, 0), 31);
+  // K = min(prec, 32) - 1 clamped to 0 = clamp(E + cexp - 1, 0, min(maxprec, 32) - 1); the block is a single bit
+  // when prec = 0, i.e. E + cexp <= 0 or maxprec = 0
+  const int ep = (int)E + cexp, kmax = min(maxprec, 32) - 1;  // kmax < 0: maxprec = 0, every block one bit
+  K = (uint32_t)max(min(ep - 1, kmax), 0);
   const float s = __uint_as_float(0x8d800000u - (m & 0x7f800000u));  // 2^(30 - emax)
   // every value of a block with E < 29 casts to INT_MIN (the scale overflows; x86 cvttss2si, encode.c:162-187):
   // an integer mask selects it per value (v_bfi), no compare-to-mask selects
@@ -103,7 +105,7 @@ __device__ __forceinline__ uint32_t v1_prep(const float* f, int cexp, int maxpre
   u[1] = (y + NB) ^ NB;
   u[2] = (z + NB) ^ NB;
   u[3] = (w + NB) ^ NB;
-  const bool one = m == 0 || prec == 0;  // a single 0 bit (encode.c:471-475)
+  const bool one = m == 0 || ep <= 0 || kmax < 0;  // a single 0 bit (encode.c:471-475; prec = 0)
   hdr = one ? 0u : 2u * E + 3u;
   // encode_ints' length from the leading planes (codec_device.h encode_ints_length, B = 4), integer-only:
   //   4 + 4 K - sum_{j<3} c_j + sum_{j<3} e_j,  c_j = min(z_j, K + 1), z_j = ffbh(S_j) of the suffix OR S_j,
