@@ -828,15 +828,16 @@ struct BitReader {
   __device__ __forceinline__ void skip(uint64_t k) { pos += k; }
 };
 
-// Reader over one block's 32-bit words staged in LDS (two zero pad words after the block).
+// Reader over 32-bit words staged in LDS (two zero pad words after the last one read): a 32-bit position (a staged
+// span is at most 2^16 words), and the 64-bit peek as two funnel shifts of three words (v_alignbit_b32).
 struct WordBitReader {
   const uint32_t* w;
-  uint64_t pos;
+  uint32_t pos;
   __device__ __forceinline__ uint64_t peek64() const
   {
-    const uint32_t i = (uint32_t)(pos >> 5), sh = (uint32_t)(pos & 31);
-    const uint64_t v = ((uint64_t)w[i] | ((uint64_t)w[i + 1] << 32)) >> sh;
-    return sh ? v | ((uint64_t)w[i + 2] << (64 - sh)) : v;
+    const uint32_t i = pos >> 5, sh = pos & 31u;
+    const uint32_t a = w[i], b = w[i + 1], c = w[i + 2];
+    return (uint64_t)__builtin_amdgcn_alignbit(c, b, sh) << 32 | __builtin_amdgcn_alignbit(b, a, sh);
   }
   __device__ __forceinline__ uint64_t get(uint32_t n)
   {
@@ -851,7 +852,7 @@ struct WordBitReader {
     pos++;
     return b;
   }
-  __device__ __forceinline__ void skip(uint64_t k) { pos += k; }
+  __device__ __forceinline__ void skip(uint64_t k) { pos += (uint32_t)k; }
 };
 
 
@@ -871,20 +872,21 @@ __device__ __forceinline__ uint32_t decode_ints(Rd& r, uint32_t maxbits, uint32_
     bits -= m;
     uint64_t x = r.get(m);
     while (n < (uint32_t)B && bits) {
-      bits--;
-      if (!r.bit()) break;  // negative group test
-      const uint32_t lim = min((uint32_t)B - 1 - n, bits);  // zeros the scan may read
+      // one peek per group test: bit 0 the test, bits 1..63 the unary scan after it
       const uint64_t w = r.peek64();
-      const uint32_t z = w ? (uint32_t)__builtin_ctzll(w) : 64u;
-      if (z < lim) {  // zeros, then the one-bit
-        r.skip(z + 1);
-        bits -= z + 1;
-        n += z;
-      } else {  // scan ran into the last coefficient or the budget: the one is implied
-        r.skip(lim);
-        bits -= lim;
-        n += lim;
+      bits--;
+      if (!(w & 1u)) {  // negative group test
+        r.skip(1);
+        break;
       }
+      const uint32_t lim = min((uint32_t)B - 1 - n, bits);  // zeros the scan may read
+      const uint64_t s = w >> 1;
+      const uint32_t z = s ? (uint32_t)__builtin_ctzll(s) : 64u;
+      // zeros, then the one-bit; or the scan ran into the last coefficient or the budget: the one is implied
+      const uint32_t adv = z < lim ? z + 1 : lim;
+      r.skip(1 + adv);
+      bits -= adv;
+      n += min(z, lim);
       x += 1ull << n;
       n++;
     }
@@ -907,20 +909,20 @@ __device__ __forceinline__ void decode_planes64(Rd& r, int kmin, uint32_t& bits,
       bits -= m;
       x = r.get(m);
       while (n < 64u && bits) {
-        bits--;
-        if (!r.bit()) break;  // negative group test
-        const uint32_t lim = min(63u - n, bits);
+        // one peek per group test: bit 0 the test, bits 1..63 the unary scan after it
         const uint64_t w = r.peek64();
-        const uint32_t z = w ? (uint32_t)__builtin_ctzll(w) : 64u;
-        if (z < lim) {
-          r.skip(z + 1);
-          bits -= z + 1;
-          n += z;
-        } else {
-          r.skip(lim);
-          bits -= lim;
-          n += lim;
+        bits--;
+        if (!(w & 1u)) {  // negative group test
+          r.skip(1);
+          break;
         }
+        const uint32_t lim = min(63u - n, bits);
+        const uint64_t s = w >> 1;
+        const uint32_t z = s ? (uint32_t)__builtin_ctzll(s) : 64u;
+        const uint32_t adv = z < lim ? z + 1 : lim;  // zeros + the one-bit, or up to the implied one
+        r.skip(1 + adv);
+        bits -= adv;
+        n += min(z, lim);
         x += 1ull << n;
         n++;
       }

@@ -246,7 +246,7 @@ __global__ __launch_bounds__(64) void k_decode_staged(FieldDesc F, Params p, con
   float f[B];
   uint64_t end;
   if (staged) {
-    WordBitReader r{sw, start_of(b) - 32 * w0};
+    WordBitReader r{sw, (uint32_t)(start_of(b) - 32 * w0)};
     decode_block<D>(r, p, f);
     end = r.pos + 32 * w0;
   } else {
