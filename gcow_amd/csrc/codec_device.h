@@ -859,6 +859,18 @@ struct WordBitReader {
 // decode_ints (libzfp 0.5.5; sw/src/decode.c:141-183 with block size 4^d). The unary scan of each group test
 // (`for (; n < size - 1 && bits && (bits--, !read_bit()); n++)`) is done with one count-trailing-zeros of the next
 // 64 stream bits instead of bit by bit.
+// Zeros before the first one-bit among bits 1..63 of w, 63 when there is none (>= any scan limit): bits 1..63 as two
+// funnel shifts with a sentinel one above them, then v_ffbl on each half (all ones for 0).
+__device__ __forceinline__ uint32_t scan_zeros63(uint64_t w)
+{
+  const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+  const uint32_t slo = __builtin_amdgcn_alignbit(hi, lo, 1u), shi = __builtin_amdgcn_alignbit(1u, hi, 1u);
+  uint32_t zl, zh;
+  asm("v_ffbl_b32 %0, %1" : "=v"(zl) : "v"(slo));
+  asm("v_ffbl_b32 %0, %1" : "=v"(zh) : "v"(shi));
+  return min(zl, zh + 32u);
+}
+
 template <int B, class Rd>
 __device__ __forceinline__ uint32_t decode_ints(Rd& r, uint32_t maxbits, uint32_t maxprec, uint32_t* u)
 {
@@ -917,8 +929,7 @@ __device__ __forceinline__ void decode_planes64(Rd& r, int kmin, uint32_t& bits,
           break;
         }
         const uint32_t lim = min(63u - n, bits);
-        const uint64_t s = w >> 1;
-        const uint32_t z = s ? (uint32_t)__builtin_ctzll(s) : 64u;
+        const uint32_t z = scan_zeros63(w);
         const uint32_t adv = z < lim ? z + 1 : lim;  // zeros + the one-bit, or up to the implied one
         r.skip(1 + adv);
         bits -= adv;
