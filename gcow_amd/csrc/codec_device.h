@@ -89,6 +89,41 @@ __device__ __forceinline__ int32_t cast1(float x, float scale)
   return (__builtin_fabsf(p) < 2147483648.0f) ? (int32_t)p : (int32_t)0x80000000;
 }
 
+// block_emax + the cast (encode.c:128-187) for a block without Inf or NaN, in about two operations per value (the
+// two-pass 3-D tile kernels; the fixed-rate kernel keeps block_emax + cast1, whose register allocation it is tuned
+// to): max |x| as the larger of an unsigned and a signed max over the bit patterns (the largest negative magnitude,
+// the largest positive value: v_max3, no per-value masking), then one fma + the hardware truncating conversion per
+// value. A finite block's products 2^(30 - emax) x lie below 2^30 in magnitude, so the conversion matches
+// cvttss2si; with an infinite scale (emax <= -98, zero blocks included) x86 gives INT_MIN for every value, here
+// fma(x, 0, -inf) -> saturated INT_MIN. Returns false when the block holds Inf or NaN (the caller takes block_emax
+// + cast1).
+template <int B>
+__device__ __forceinline__ bool emax_cast_finite(const float* fa, int& emax, int32_t* q)
+{
+  uint32_t mu = 0;
+  int32_t mi = 0;
+#pragma unroll
+  for (int i = 0; i < B; i += 2) {
+    const uint32_t a = __float_as_uint(fa[i]), b = __float_as_uint(fa[i + 1]);
+    mu = max(mu, max(a, b));
+    mi = max(mi, max((int32_t)a, (int32_t)b));
+  }
+  const uint32_t m = max(mu & 0x7fffffffu, (uint32_t)mi & 0x7fffffffu);
+  if (m >= 0x7f800000u) return false;
+  emax = m == 0 ? -127 : max((int)(m >> 23) - 126, -126);
+  const int se = 30 - emax;
+  const bool tiny = se >= 128;
+  const float s = tiny ? 0.0f : __uint_as_float((uint32_t)(se + 127) << 23);
+  const float c = tiny ? -__builtin_inff() : 0.0f;
+#pragma unroll
+  for (int i = 0; i < B; i++) {
+    int32_t v;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(v) : "v"(__builtin_fmaf(fa[i], s, c)));
+    q[i] = v;
+  }
+  return true;
+}
+
 // fwd_lift_vector (encode.c:189-249), int32 wraparound made explicit.
 __device__ __forceinline__ void fwd_lift(int32_t& x, int32_t& y, int32_t& z, int32_t& w)
 {
@@ -722,14 +757,19 @@ __device__ __forceinline__ uint32_t count_block(const float* f, const Params& p)
   float fa[B];
 #pragma unroll
   for (int i = 0; i < B; i++) fa[i] = f[i];
-  const int emax = block_emax<B>(fa);
+  int emax = 0;
+  int32_t q[B];
+  bool fast = false;
+  if constexpr (B == 64) fast = emax_cast_finite<B>(fa, emax, q);
+  if (!fast) emax = block_emax<B>(fa);
   const uint32_t prec = precision(emax, p.maxprec, p.minexp, D);
   const uint32_t be = prec ? (uint32_t)(emax + 127) : 0u;
   if (!be) return p.minbits > 1u ? p.minbits : 1u;
-  int32_t q[B];
-  const float s = cast_scale(emax);
+  if (!fast) {
+    const float s = cast_scale(emax);
 #pragma unroll
-  for (int i = 0; i < B; i++) q[i] = cast1(fa[i], s);
+    for (int i = 0; i < B; i++) q[i] = cast1(fa[i], s);
+  }
   fwd_xform<D>(q);
   uint32_t u[B];
   fwd_reorder<D>(u, q);
@@ -758,14 +798,19 @@ __device__ __forceinline__ BlockHead prepare_block(const float* f, const Params&
   float fa[B];
 #pragma unroll
   for (int i = 0; i < B; i++) fa[i] = f[i];
-  const int emax = block_emax<B>(fa);
+  int emax = 0;
+  int32_t q[B];
+  bool fast = false;
+  if constexpr (B == 64) fast = emax_cast_finite<B>(fa, emax, q);
+  if (!fast) {
+    emax = block_emax<B>(fa);
+    const float s = cast_scale(emax);
+#pragma unroll
+    for (int i = 0; i < B; i++) q[i] = cast1(fa[i], s);
+  }
   BlockHead h;
   h.prec = precision(emax, p.maxprec, p.minexp, D);
   h.be = h.prec ? (uint32_t)(emax + 127) : 0u;
-  int32_t q[B];
-  const float s = cast_scale(emax);
-#pragma unroll
-  for (int i = 0; i < B; i++) q[i] = cast1(fa[i], s);
   fwd_xform<D>(q);
   fwd_reorder<D>(u, q);
   const uint32_t maxb = p.maxbits - 9u;
@@ -839,10 +884,11 @@ struct WordBitReader {
     const uint32_t a = w[i], b = w[i + 1], c = w[i + 2];
     return (uint64_t)__builtin_amdgcn_alignbit(c, b, sh) << 32 | __builtin_amdgcn_alignbit(b, a, sh);
   }
-  __device__ __forceinline__ uint64_t get(uint32_t n)
+  __device__ __forceinline__ uint64_t get(uint32_t n)  // n <= 64
   {
     if (!n) return 0;
-    uint64_t v = peek64() & lowmask64(n);
+    const uint32_t k = 64u - n;
+    const uint64_t v = (peek64() << k) >> k;
     pos += n;
     return v;
   }

@@ -915,6 +915,36 @@ def test_fixed3d_word_rates(gc, orc, r):
     _check_vs_oracle(gc, orc, bf, orc.rate(r, 3), decode=False)
 
 
+@pytest.mark.parametrize("mode", ["acc", "prec", "rate"])
+def test_3d_emax_cast_edge_blocks(gc, orc, mode):
+    """The 64-value finite-block prologue (codec_device.h emax_cast_finite: max |x| from unsigned and signed maxima of
+    the bit patterns, fma + truncating conversion, INT_MIN for an infinite scale) against the oracle on the blocks it
+    must get right: all-negative and all-positive blocks, -0.0, subnormal-only, tiny (scale overflow), maxima at
+    2^k and just below, largest finite values, and Inf / NaN blocks (the generic path); fixed rate, accuracy and
+    precision, fp32 and bf16."""
+    rng = np.random.default_rng(3)
+    a = (rng.standard_normal((16, 16, 12)) * 1e-2).astype(np.float32)
+    a[:4, :4, :4] = -np.abs(a[:4, :4, :4])           # all negative
+    a[:4, 4:8, :4] = np.abs(a[:4, 4:8, :4])          # all positive
+    a[:4, 8:12, :4] = -0.0                           # negative zeros
+    a[:4, 12:16, :4] = 1e-40                         # subnormal only
+    a[4:8, :4, :4] = -3e-37                          # tiny, negative
+    a[4:8, 4:8, :4] *= 1e-30                         # small normal
+    a[4:8, 8:12, :4] = 1.0
+    a[4:8, 8:12, 0] = -2.0                           # negative power-of-two maximum
+    a[4:8, 12:16, :4] = np.float32(np.nextafter(np.float32(4.0), np.float32(0.0)))
+    a[8:12, :4, :4] = np.finfo(np.float32).max * np.sign(a[8:12, :4, :4])
+    a[8:12, 4:8, :4] = np.float32(-np.finfo(np.float32).tiny)
+    a[8, 9, 1] = np.inf
+    a[9, 13, 2] = -np.inf
+    a[13, 2, 5] = np.nan
+    a[14, 6, 9] = -np.nan
+    p = {"acc": orc.accuracy(1e-3), "prec": orc.precision(20), "rate": orc.rate(8, 3)}[mode]
+    _check_vs_oracle(gc, orc, a, p)
+    bf = (a.view(np.uint32) >> 16).astype(np.uint16)
+    _check_vs_oracle(gc, orc, bf, p, decode=False)
+
+
 @pytest.mark.parametrize("shape", [(12, 12, 12), (40, 44), (4 * 4099 + 1,)])
 def test_staged_decode_wide_blocks(gc, orc, shape):
     """LDS-staged decoders with spans over their capacity (precision 32 on values spread over 2^-60..2^10: blocks of
