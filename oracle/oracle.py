@@ -98,6 +98,8 @@ def _bind(L):
                                    P(C.c_uint64), C.c_size_t]
         L.orc_compress_mt.restype = C.c_uint64
         L.orc_compress_mt.argtypes = L.orc_compress.argtypes + [C.c_int]
+        L.orc_compress_mt_off.restype = C.c_uint64
+        L.orc_compress_mt_off.argtypes = L.orc_compress.argtypes + [C.c_int, P(C.c_uint64)]
         L.orc_block_bits.argtypes = [C.c_void_p, C.c_int, C.c_uint, P(C.c_size_t), P(C.c_ssize_t), P(Params),
                                      P(C.c_uint32)]
         L.orc_decompress.restype = C.c_uint64
@@ -111,6 +113,8 @@ def _bind(L):
         L.orc_gen_normal.argtypes = [P(C.c_float), C.c_size_t, C.c_double, C.c_uint64, C.c_int]
         L.orc_decompress_at.restype = C.c_uint64
         L.orc_decompress_at.argtypes = L.orc_decompress.argtypes + [C.c_uint64]
+        L.orc_decompress_mt.restype = C.c_uint64
+        L.orc_decompress_mt.argtypes = L.orc_decompress.argtypes + [C.c_int, P(C.c_uint64)]
         L.orc_stitch.argtypes = [P(C.c_uint64), C.c_uint64, P(C.c_uint64), C.c_uint64]
         L.orc_header_bits.restype = C.c_uint
         L.orc_header_bits.argtypes = [P(Params)]
@@ -195,8 +199,9 @@ def max_words(shape, p: Params) -> int:
     return (nb * mb + 63) // 64 + 2
 
 
-def compress(arr: np.ndarray, p: Params, threads: int = 0, L=None):
-    """Encode a C-contiguous float32 (or bf16-as-uint16) array. Returns (words[uint64], total_bits)."""
+def compress(arr: np.ndarray, p: Params, threads: int = 0, L=None, offsets: bool = False):
+    """Encode a C-contiguous float32 (or bf16-as-uint16) array. Returns (words[uint64], total_bits), plus (offsets)
+    the threaded encode's shard start bits (uint64[T + 1]) that `decompress(..., threads=T, offsets=...)` resumes at."""
     arr = np.ascontiguousarray(arr)
     dtype = BF16 if arr.dtype == np.uint16 else F32
     if dtype == F32:
@@ -205,12 +210,21 @@ def compress(arr: np.ndarray, p: Params, threads: int = 0, L=None):
     nw = max_words(arr.shape, p)
     out = np.zeros(nw, dtype=np.uint64)
     L = L or lib()
-    if threads and threads > 1:
+    offs = None
+    if offsets:
+        T = max(1, threads or 1)
+        offs = np.zeros(T + 1, np.uint64)
+        bits = L.orc_compress_mt_off(arr.ctypes.data, dtype, dims, n, None, C.byref(p), _p(out, C.c_uint64), nw, T,
+                                     _p(offs, C.c_uint64))
+        nb = lib().orc_num_blocks(dims, n)
+        offs = offs[: min(T, max(nb, 1)) + 1].copy()
+    elif threads and threads > 1:
         bits = L.orc_compress_mt(arr.ctypes.data, dtype, dims, n, None, C.byref(p), _p(out, C.c_uint64), nw,
                                  threads)
     else:
         bits = L.orc_compress(arr.ctypes.data, dtype, dims, n, None, C.byref(p), _p(out, C.c_uint64), nw)
-    return out[: (bits + 63) // 64].copy(), int(bits)
+    w = out[: (bits + 63) // 64].copy()
+    return (w, int(bits), offs) if offsets else (w, int(bits))
 
 
 def block_bits(arr: np.ndarray, p: Params) -> np.ndarray:
@@ -223,12 +237,21 @@ def block_bits(arr: np.ndarray, p: Params) -> np.ndarray:
     return out
 
 
-def decompress(words: np.ndarray, shape, p: Params) -> np.ndarray:
+def decompress(words: np.ndarray, shape, p: Params, threads: int = 0, offsets=None) -> np.ndarray:
+    """Decode into a float32 array of `shape`. threads > 1 splits the blocks as the threaded encode does: each shard
+    starts at offsets[t] (from compress(..., offsets=True) with the same thread count), or at t * per * maxbits for a
+    fixed-rate stream when offsets is None."""
     dims, n = _shape(shape)
     out = np.zeros(shape, dtype=np.float32)
     w = np.ascontiguousarray(words, dtype=np.uint64)
     w = np.concatenate([w, np.zeros(2, np.uint64)])
-    lib().orc_decompress(_p(out, C.c_float), dims, n, None, C.byref(p), _p(w, C.c_uint64), len(w))
+    if threads and threads > 1 and (offsets is not None or p.minbits == p.maxbits):
+        T = len(offsets) - 1 if offsets is not None else threads
+        offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+        lib().orc_decompress_mt(_p(out, C.c_float), dims, n, None, C.byref(p), _p(w, C.c_uint64), len(w), T,
+                                None if offs is None else _p(offs, C.c_uint64))
+    else:
+        lib().orc_decompress(_p(out, C.c_float), dims, n, None, C.byref(p), _p(w, C.c_uint64), len(w))
     return out
 
 

@@ -544,12 +544,27 @@ static void stitch(uint64_t* out, uint64_t off, const uint64_t* src, uint64_t bi
 
 void orc_stitch(uint64_t* out, uint64_t off, const uint64_t* src, uint64_t bits) { stitch(out, off, src, bits); }
 
+static int clamp_threads(int nthreads, size_t nb)
+{
+  if (nthreads < 1) nthreads = 1;
+  if ((size_t)nthreads > nb) nthreads = (int)(nb ? nb : 1);
+  return nthreads;
+}
+
 uint64_t orc_compress_mt(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
                          const orc_params* p, uint64_t* out, size_t out_words, int nthreads)
 {
+  return orc_compress_mt_off(data, dtype, dims, n, s, p, out, out_words, nthreads, NULL);
+}
+
+/* Threaded encode: shard t = blocks [t * per, (t + 1) * per), per = ceil(nb / T), encoded independently and
+ * stitched in order. shard_off (optional, T + 1 entries, T = the clamped thread count) receives each shard's first
+ * bit in the stitched stream -- the split points orc_decompress_mt resumes at. */
+uint64_t orc_compress_mt_off(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
+                             const orc_params* p, uint64_t* out, size_t out_words, int nthreads, uint64_t* shard_off)
+{
   size_t nb = orc_num_blocks(dims, n);
-  if (nthreads < 1) nthreads = 1;
-  if ((size_t)nthreads > nb) nthreads = (int)(nb ? nb : 1);
+  nthreads = clamp_threads(nthreads, nb);
   shard_job* jobs = (shard_job*)calloc((size_t)nthreads, sizeof(shard_job));
   pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
   size_t per = (nb + nthreads - 1) / nthreads;
@@ -567,10 +582,12 @@ uint64_t orc_compress_mt(const void* data, int dtype, unsigned dims, const size_
   uint64_t off = 0;
   for (int t = 0; t < nthreads; t++) {
     pthread_join(th[t], NULL);
+    if (shard_off) shard_off[t] = off;
     stitch(out, off, jobs[t].buf, jobs[t].bits);
     off += jobs[t].bits;
     free(jobs[t].buf);
   }
+  if (shard_off) shard_off[nthreads] = off;
   free(jobs);
   free(th);
   return off;
@@ -691,22 +708,77 @@ uint64_t orc_decompress(float* data, unsigned dims, const size_t* n, const ptrdi
   return pos;
 }
 
+static uint64_t decompress_range(float* data, unsigned dims, const size_t* n, const ptrdiff_t* st, const orc_params* p,
+                                 const uint64_t* in, size_t first, size_t last, uint64_t pos)
+{
+  float f[256];
+  size_t b[4];
+  for (size_t i = first; i < last; i++) {
+    block_coords(i, dims, n, b);
+    decode_fblock(in, &pos, p, f, dims);
+    scatter_block(f, data, dims, n, st, b);
+  }
+  return pos;
+}
+
 uint64_t orc_decompress_at(float* data, unsigned dims, const size_t* n, const ptrdiff_t* s, const orc_params* p,
                            const uint64_t* in, size_t in_words, uint64_t start_bit)
 {
   (void)in_words;
   ptrdiff_t st[4];
   default_strides(dims, n, s, st);
+  return decompress_range(data, dims, n, st, p, in, 0, orc_num_blocks(dims, n), start_bit);
+}
+
+typedef struct {
+  float* data;
+  unsigned dims;
+  const size_t* n;
+  const ptrdiff_t* st;
+  const orc_params* p;
+  const uint64_t* in;
+  size_t first, last;
+  uint64_t pos;
+} dshard_job;
+
+static void* dshard_main(void* arg)
+{
+  dshard_job* j = (dshard_job*)arg;
+  j->pos = decompress_range(j->data, j->dims, j->n, j->st, j->p, j->in, j->first, j->last, j->pos);
+  return NULL;
+}
+
+/* Threaded decode with the shard split of orc_compress_mt_off: shard t (blocks [t * per, (t + 1) * per)) starts at
+ * bit shard_off[t]. shard_off may be NULL for fixed-rate streams (block i starts at i * maxbits). Every thread decodes
+ * with the sequential decoder; returns the end bit of the last shard. */
+uint64_t orc_decompress_mt(float* data, unsigned dims, const size_t* n, const ptrdiff_t* s, const orc_params* p,
+                           const uint64_t* in, size_t in_words, int nthreads, const uint64_t* shard_off)
+{
+  (void)in_words;
+  ptrdiff_t st[4];
+  default_strides(dims, n, s, st);
   size_t nb = orc_num_blocks(dims, n);
-  uint64_t pos = start_bit;
-  float f[256];
-  size_t b[4];
-  for (size_t i = 0; i < nb; i++) {
-    block_coords(i, dims, n, b);
-    decode_fblock(in, &pos, p, f, dims);
-    scatter_block(f, data, dims, n, st, b);
+  nthreads = clamp_threads(nthreads, nb);
+  if (!shard_off && p->minbits != p->maxbits) nthreads = 1;
+  size_t per = (nb + nthreads - 1) / nthreads;
+  dshard_job* jobs = (dshard_job*)calloc((size_t)nthreads, sizeof(dshard_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; t++) {
+    dshard_job* j = &jobs[t];
+    j->data = data; j->dims = dims; j->n = n; j->st = st; j->p = p; j->in = in;
+    j->first = OMIN(nb, (size_t)t * per);
+    j->last = OMIN(nb, j->first + per);
+    j->pos = shard_off ? shard_off[t] : (uint64_t)j->first * p->maxbits;
+    pthread_create(&th[t], NULL, dshard_main, j);
   }
-  return pos;
+  uint64_t end = 0;
+  for (int t = 0; t < nthreads; t++) {
+    pthread_join(th[t], NULL);
+    end = jobs[t].pos;
+  }
+  free(jobs);
+  free(th);
+  return end;
 }
 
 /* ------------------------------------------------------------------------------------------------

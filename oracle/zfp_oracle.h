@@ -57,6 +57,9 @@ uint64_t orc_compress(const void* data, int dtype, unsigned dims, const size_t* 
 /* Threaded CPU baseline: block-aligned shards encoded into private streams, then serial bit-stitch. */
 uint64_t orc_compress_mt(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
                          const orc_params* p, uint64_t* out, size_t out_words, int nthreads);
+/* The same, with each shard's first bit in shard_off[0 .. T] (T = min(nthreads, nblocks); shard_off[T] = end). */
+uint64_t orc_compress_mt_off(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
+                             const orc_params* p, uint64_t* out, size_t out_words, int nthreads, uint64_t* shard_off);
 /* Per-block bit lengths (for offset checks). */
 void orc_block_bits(const void* data, int dtype, unsigned dims, const size_t* n, const ptrdiff_t* s,
                     const orc_params* p, uint32_t* bits_out);
@@ -66,6 +69,9 @@ uint64_t orc_decompress(float* data, unsigned dims, const size_t* n, const ptrdi
 
 uint64_t orc_decompress_at(float* data, unsigned dims, const size_t* n, const ptrdiff_t* s, const orc_params* p,
                            const uint64_t* in, size_t in_words, uint64_t start_bit);
+/* Threaded decode over the shards of orc_compress_mt_off (shard_off NULL: fixed rate). */
+uint64_t orc_decompress_mt(float* data, unsigned dims, const size_t* n, const ptrdiff_t* s, const orc_params* p,
+                           const uint64_t* in, size_t in_words, int nthreads, const uint64_t* shard_off);
 /* OR `bits` bits of src into zeroed out[] at bit offset off (the multi-shard stream stitch). */
 void orc_stitch(uint64_t* out, uint64_t off, const uint64_t* src, uint64_t bits);
 

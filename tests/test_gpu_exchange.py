@@ -122,6 +122,42 @@ def test_decode_mean_vs_oracle(gc, orc, mode, world):
     assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.parametrize("mode", ["rate16", "acc1e-6"])
+def test_decode_mean_full_size_w8(gc, orc, mode):
+    """The hook's receive side at the bench's size: 8 streams of 256 Mi fp32 values (8 different buckets, the bench's
+    fill_normal with seeds 0x67636F77 + r) decoded and averaged in one launch == the threaded oracle decodes summed
+    in rank order in fp32, divided by 8, over the whole bucket."""
+    W, n = 8, 256 * 1024 * 1024
+    T = min(16, os.cpu_count() or 1)
+    op = orc.rate(16, 1) if mode == "rate16" else orc.accuracy(1e-6)
+    fixed = op.minbits == op.maxbits
+    p = _P(gc, op)
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    enc = gc.Encoder((n,), torch.float32, p, index_stride=0 if fixed else 16)
+    acc = np.zeros(n, np.float32)
+    parts, idx = [], []
+    for r in range(W):
+        gc.fill_normal(x, 1e-3, seed=0x67636F77 + r, inject=True)
+        e = enc(x)
+        parts.append(e.stream().clone())
+        if not fixed:
+            idx.append(e.index.clone())
+        w_ref, bits, offs = orc.compress(x.cpu().numpy(), op, threads=T, offsets=True)
+        assert e.bits == bits
+        acc = acc + orc.decompress(w_ref, (n,), op, threads=T, offsets=None if fixed else offs)
+        del w_ref
+    want = acc / np.float32(W)
+    del acc
+    sw = max(s.numel() for s in parts)
+    streams = torch.zeros(W * sw + 2, dtype=torch.int64, device="cuda")
+    for r, s in enumerate(parts):
+        streams[r * sw:r * sw + s.numel()] = s
+    ni = idx[0].numel() if idx else 0
+    got = gc.decode_mean(streams, sw, W, n, p, torch.cat(idx) if idx else None, ni, 0 if fixed else 16, out=x)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
 def test_decode_mean_argument_checks(gc, orc):
     """The C entry validates what its kernels assume: 2 readable words past the last stream, and no block index on
     the fixed-rate path."""

@@ -173,6 +173,25 @@ def test_threaded_equals_serial(orc):
         assert b1 == b2 and np.array_equal(w1, w2)
 
 
+@pytest.mark.parametrize("shape,mode", [((1 << 16) + 3, "acc1e-6"), ((1 << 16) + 3, "rate16"), ((37, 41, 45), "acc1e-3"),
+                                        ((37, 41, 45), "rate8"), ((100, 99), "prec20"), ((5,), "acc1e-6")])
+def test_threaded_decode_equals_serial(orc, shape, mode):
+    """The threaded oracle decode (the full-size GPU decode checks use it) equals the serial decode: variable rate
+    from the threaded encode's shard offsets, fixed rate from block positions; more threads than blocks too."""
+    shape = shape if isinstance(shape, tuple) else (shape,)
+    dims = len(shape)
+    p = {"acc1e-6": orc.accuracy(1e-6), "acc1e-3": orc.accuracy(1e-3), "rate16": orc.rate(16, dims),
+         "rate8": orc.rate(8, dims), "prec20": orc.precision(20)}[mode]
+    a = orc.gen_normal(int(np.prod(shape)), 1e-3, 5, True).reshape(shape)
+    w, b = orc.compress(a, p)
+    w2, b2, offs = orc.compress(a, p, threads=7, offsets=True)
+    assert b2 == b and np.array_equal(w2, w) and int(offs[-1]) == b and int(offs[0]) == 0
+    ref = orc.decompress(w, shape, p).view(np.uint32)
+    assert np.array_equal(orc.decompress(w, shape, p, threads=7, offsets=offs).view(np.uint32), ref)
+    if p.minbits == p.maxbits:
+        assert np.array_equal(orc.decompress(w, shape, p, threads=5).view(np.uint32), ref)
+
+
 def test_block_bits_sum(orc):
     a = orc.gen_normal(4099, inject=True)
     p = orc.accuracy(1e-6)

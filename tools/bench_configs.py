@@ -109,7 +109,43 @@ def var_decode():
     for tol in (1e-6, 1e-3):
         e = codec.encode(x, codec.accuracy(tol), index_stride=16)
         ms = timeit(lambda: codec.decode(e, out=out), reps=3)
-        emit(case="var_decode_f32_acc%g" % tol, ms=round(ms, 3), GiBps_output=round(n * 4 / (ms / 1e3) / 2 ** 30, 1))
+        emit(case="var_decode_f32_acc%g" % tol, ms=round(ms, 3), GiBps_output=round(n * 4 / (ms / 1e3) / 2 ** 30, 1),
+             bits_per_value=round(e.bits / n, 3))
+    xb = x.to(torch.bfloat16)
+    e = codec.encode(xb, codec.accuracy(1e-6), index_stride=16)
+    ms = timeit(lambda: codec.decode(e, out=out), reps=3)
+    emit(case="var_decode_bf16src_acc1e-06", ms=round(ms, 3), GiBps_output=round(n * 4 / (ms / 1e3) / 2 ** 30, 1),
+         bits_per_value=round(e.bits / n, 3))
+
+
+def decode_mean(W=8):
+    """The receive side of the compressed all-gather hook on one GPU: W streams of 256 Mi fp32 values (W different
+    buckets) decoded and averaged in one launch (codec.decode_mean), rate 16 and accuracy 1e-6."""
+    n = 256 << 20
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    out = torch.empty_like(x)
+    for name, p, stride in (("rate16", codec.rate(16, 1), 0), ("acc1e-6", codec.accuracy(1e-6), 16)):
+        enc = codec.Encoder((n,), torch.float32, p, index_stride=stride)
+        streams, idx, lens = [], [], []
+        for r in range(W):
+            codec.fill_normal(x, 1e-3, seed=0x67636F77 + r)
+            e = enc(x)
+            streams.append(e.stream().clone())
+            idx.append(e.index.clone() if e.index is not None else None)
+            lens.append(e.bits)
+        sw = max(s.numel() for s in streams)
+        buf = torch.zeros(W * sw + 2, dtype=torch.int64, device="cuda")
+        for r, s in enumerate(streams):
+            buf[r * sw:r * sw + s.numel()] = s
+        ix = torch.cat(idx) if stride else None
+        ni = idx[0].numel() if stride else 0
+        ms = timeit(lambda: codec.decode_mean(buf, sw, W, n, p, ix, ni, stride, out=out), reps=3)
+        cbytes = sum(lens) / 8
+        emit(case="decode_mean_%s_W%d" % (name, W), ms=round(ms, 3),
+             GBps_write=round(n * 4 / (ms / 1e3) / 1e9, 1),
+             GBps_read_write=round((n * 4 + cbytes) / (ms / 1e3) / 1e9, 1),
+             bits_per_value=round(sum(lens) / W / n, 3))
+        del buf, streams, idx, enc
 
 
 def c5():

@@ -68,6 +68,44 @@ def c5(reps):
         torch.cuda.synchronize()
 
 
+def vdec(reps):
+    """1-D variable-rate decode (accuracy 1e-6, block index every 16 blocks) of the fp32 and the bf16 C5 bucket."""
+    n = 256 << 20
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    codec.fill_normal(x)
+    out = torch.empty_like(x)
+    for src in (x, x.to(torch.bfloat16)):
+        e = codec.encode(src, codec.accuracy(1e-6), index_stride=16)
+        for _ in range(reps):
+            codec.decode(e, out=out)
+        torch.cuda.synchronize()
+
+
+def dmean(reps, W=8):
+    """decode_mean over W streams of 256 Mi values: rate 16, then accuracy 1e-6."""
+    n = 256 << 20
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    out = torch.empty_like(x)
+    for p, stride in ((codec.rate(16, 1), 0), (codec.accuracy(1e-6), 16)):
+        enc = codec.Encoder((n,), torch.float32, p, index_stride=stride)
+        ss, ix = [], []
+        for r in range(W):
+            codec.fill_normal(x, 1e-3, seed=0x67636F77 + r)
+            e = enc(x)
+            ss.append(e.stream().clone())
+            ix.append(e.index.clone() if stride else None)
+        sw = max(s.numel() for s in ss)
+        buf = torch.zeros(W * sw + 2, dtype=torch.int64, device="cuda")
+        for r, s in enumerate(ss):
+            buf[r * sw:r * sw + s.numel()] = s
+        idx = torch.cat(ix) if stride else None
+        ni = ix[0].numel() if stride else 0
+        for _ in range(reps):
+            codec.decode_mean(buf, sw, W, n, p, idx, ni, stride, out=out)
+        torch.cuda.synchronize()
+        del buf, ss, ix, enc
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("cases", nargs="*", default=["c3", "c5"])
