@@ -60,6 +60,8 @@ def parse(argv=None):
     ap.add_argument("--no-extras", action="store_true", help="only the headline measurement")
     ap.add_argument("--stub", action="store_true",
                     help="harness self-test on CPU: gloo, a trivial step instead of the encode (tests only)")
+    ap.add_argument("--stub-mismatch", action="store_true",
+                    help="stub mode: report a failed oracle check (tests that the run then exits non-zero)")
     ap.add_argument("--multi-legs", action="store_true",
                     help="run the N > 1 legs (exchange, subgroups, strong, c5_sharded) even at N = 1, over a one-rank "
                          "RCCL group (tests: exercises the multi-GPU code on a one-GPU box)")
@@ -587,6 +589,35 @@ def cpu_baseline(x: torch.Tensor, rate: float, dev) -> dict:
 
 
 # ------------------------------------------------------------------------------------------------------ main
+def parity_failures(obj, path="") -> list:
+    """Paths of every `*_matches_oracle` flag in the bench line that is False (None = not checked on this rank)."""
+    bad = []
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            if k.endswith("_matches_oracle") and v is False:
+                bad.append(path + k)
+            else:
+                bad += parity_failures(v, path + k + ".")
+    elif isinstance(obj, list):
+        for i, v in enumerate(obj):
+            bad += parity_failures(v, "%s%d." % (path, i))
+    return bad
+
+
+def finish(ctx: Ctx, line) -> int:
+    """Print the JSON line (rank 0), tear down the group, and return the exit code: 3 when an oracle check in the
+    line failed, so a stitch / shard-offset bug on the driver's N-rank run is an rc != 0, not a `false` in a tail."""
+    bad = []
+    if line is not None:
+        print(json.dumps(line), flush=True)
+        bad = parity_failures(line)
+        if bad:
+            print("bench.py: ORACLE CHECK FAILED: %s" % ", ".join(bad), file=sys.stderr, flush=True)
+    if ctx.group:
+        dist.destroy_process_group()
+    return 3 if bad else 0
+
+
 def stub_worker(ctx: Ctx):
     """Harness self-test (tests/test_bench_launcher.py): the same timing / max-over-ranks / JSON path with a trivial
     CPU step."""
@@ -599,19 +630,19 @@ def stub_worker(ctx: Ctx):
         dist.all_gather_object(ranks, me)
     else:
         ranks = [me]
+    line = None
     if ctx.rank == 0:
-        print(json.dumps({"metric": METRIC, "value": round(gib(ctx.world * ctx.args.values * 4, wall), 3),
-                          "unit": "GiB/s", "n_gpus": ctx.world, "steps": ctx.args.steps, "warmup": ctx.args.warmup,
-                          "ms_per_step": round(wall, 5), "data": "stub", "ranks": ranks}), flush=True)
+        line = {"metric": METRIC, "value": round(gib(ctx.world * ctx.args.values * 4, wall), 3),
+                "unit": "GiB/s", "n_gpus": ctx.world, "steps": ctx.args.steps, "warmup": ctx.args.warmup,
+                "ms_per_step": round(wall, 5), "data": "stub", "ranks": ranks,
+                "stub_check": {"stream_matches_oracle": not ctx.args.stub_mismatch}}
+    return finish(ctx, line)
 
 
 def worker(args):
     ctx = Ctx(args)
     if ctx.stub:
-        stub_worker(ctx)
-        if ctx.world > 1:
-            dist.destroy_process_group()
-        return
+        return stub_worker(ctx)
     from gcow_amd import codec  # after the device is set: libgcow.so shares torch's HIP runtime
 
     n = args.values
@@ -691,6 +722,7 @@ def worker(args):
             cpu = {"error": repr(ex)}
             print("bench.py: cpu_baseline failed: %r" % (ex,), file=sys.stderr)
 
+    line = None
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -713,9 +745,7 @@ def worker(args):
             "cpu_baseline": cpu,
         }
         line.update(extra)
-        print(json.dumps(line), flush=True)
-    if ctx.group:
-        dist.destroy_process_group()
+    return finish(ctx, line)
 
 
 def main(argv=None):
@@ -723,7 +753,7 @@ def main(argv=None):
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(args, argv))
-    worker(args)
+    sys.exit(worker(args))
 
 
 if __name__ == "__main__":

@@ -115,6 +115,7 @@ def load():
         "gcow_decode_device_at": (i32, [pi, pp, vp, sz, u64, vp, u32, vp]),
         "gcow_fill_normal_device": (i32, [vp, sz, C.c_double, u64, i32, vp]),
         "gcow_copy_pattern_device": (i32, [vp, i32, sz, u32, vp, vp]),
+        "gcow_debug_set_var1d_variant": (i32, [i32, i32, i32]),
         "gcow_stage_emax_device": (i32, [vp, u32, u32, vp, vp]),
         "gcow_stage_cast_device": (i32, [vp, vp, u32, u32, vp, vp]),
         "gcow_stage_xform_device": (i32, [vp, u32, u32, i32, vp]),

@@ -7,6 +7,7 @@ memory and streams; every byte of codec work runs in the gfx950 kernels of gcow_
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import math
 from dataclasses import dataclass
@@ -175,7 +176,7 @@ def field_of_shape(shape, dtype) -> ZfpInput:
 def encode(x: torch.Tensor, params: GcowParams, index_stride: int = 0, stream=None) -> Encoded:
     """zfp_compress of a device tensor (1-4 dims, fp32 or bf16, any strides)."""
     if not x.is_cuda:
-        raise GcowError("encode expects a device tensor (use gcow_amd.dropin for host arrays)")
+        raise GcowError("encode expects a device tensor (host arrays: the sw/ drop-in zfp_compress in libgcow.so, see INTEGRATION.md; or codec.HostEncoder for a pinned 1-D bucket)")
     enc = Encoder(x.shape, x.dtype, params, x.device, index_stride)
     L = enc.L
     f = field_of(x)
@@ -274,6 +275,22 @@ def c3_field(device=None, side: int = 512, seed: int = 21) -> torch.Tensor:
     f = f.view(side, side, side).mul_(1e-3)
     f += sx[None, None, :] * cy[None, :, None] * sz[:, None, None]
     return f.contiguous()
+
+
+VAR1D_FORMS = {"tile": 0, "range": 1, "single_pass": 2}
+
+
+@contextlib.contextmanager
+def var1d_variant(form: str = "tile", spin: int = -1, stats: bool = False):
+    """TEST / MEASUREMENT ONLY: run the 1-D variable-rate encoder in one of its measured-and-not-kept forms inside the
+    `with` block (gcow_debug_set_var1d_variant; process-wide, restored to the default tile form on exit)."""
+    L = load()
+    check(L.gcow_debug_set_var1d_variant(VAR1D_FORMS[form], int(spin), int(bool(stats))),
+          "gcow_debug_set_var1d_variant")
+    try:
+        yield
+    finally:
+        check(L.gcow_debug_set_var1d_variant(0, -1, 0), "gcow_debug_set_var1d_variant")
 
 
 # ------------------------------------------------------------------------------------------- zfpy byte streams

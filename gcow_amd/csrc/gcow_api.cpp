@@ -13,6 +13,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "gcow.h"
 #include "kernels.h"
@@ -288,7 +289,7 @@ struct OutState {
   uint32_t dims = 0;
   uint64_t nblocks = 0;
   uint64_t words = 0;
-  uint64_t hash = 0;  // hash_words() of the caller's host stream when the cache was filled
+  std::vector<uint64_t> shadow;  // host streams: the caller's stream as zfp_compress left it (exact cache check)
 };
 
 std::mutex g_mu;
@@ -356,19 +357,9 @@ bool strided(const zfp_input* in) { return in->sx || in->sy || in->sz || in->sw;
 
 // Whole-stream check that the caller's buffer still holds the stream zfp_compress left in it (zfp_decompress reuses
 // the device copy only then; a caller that rewrote its buffer -- another stream of the same shape, a local edit -- is
-// decoded from its new contents). Host streams: a 64-bit hash of every word, taken at compress time and recomputed
-// at decompress time. Device streams: every word compared on the device against the cached copy.
-uint64_t hash_words(const uint64_t* w, uint64_t words)
-{
-  uint64_t h = 0x67636F77ull ^ (words * 0x9E3779B97F4A7C15ull);
-  for (uint64_t i = 0; i < words; i++) {
-    uint64_t z = w[i] + 0x9E3779B97F4A7C15ull * (i + 1);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    h = (h ^ z ^ (z >> 31)) * 0xff51afd7ed558ccdull;
-  }
-  return h ^ (h >> 33);
-}
+// decoded from its new contents). Host streams: a memcmp against a host shadow copy taken at compress time (exact, no
+// hash collisions, and faster than hashing: one memcpy at compress, one memcmp at decompress). Device streams: every
+// word compared on the device against the cached copy.
 
 // Host-side copy of `bits` bits from words src into stream s at its current write position (stream.c:61-92).
 void append_bits(stream* s, const uint64_t* src, uint64_t bits)
@@ -1018,6 +1009,13 @@ gcow_status gcow_copy_pattern_device(const void* d_in, int dtype, size_t nvals, 
   return GCOW_OK;
 }
 
+gcow_status gcow_debug_set_var1d_variant(int form, int spin, int stats)
+{
+  if (form < 0 || form > 2) return fail(GCOW_ERR_INVALID, "form: 0 tile, 1 range, 2 look-back single pass");
+  gcow::g_var1d_variant = gcow::Var1dVariant{form, spin, stats};
+  return GCOW_OK;
+}
+
 gcow_status gcow_fill_normal_device(float* d_out, size_t count, double sigma, uint64_t seed, int inject,
                                     void* hip_stream)
 {
@@ -1155,7 +1153,12 @@ size_t zfp_compress(zfp_output* output, const zfp_input* input)
     free(tmp);
     stream_flush(s);
   }
-  st->hash = dev_out ? 0 : hash_words((const uint64_t*)s->begin, words);
+  if (dev_out) {
+    st->shadow.clear();
+    st->shadow.shrink_to_fit();
+  } else {
+    st->shadow.assign((const uint64_t*)s->begin, (const uint64_t*)s->begin + words);
+  }
   st->valid = true;
   st->host_begin = s->begin;
   st->words = words;
@@ -1195,7 +1198,8 @@ size_t zfp_decompress(zfp_output* output, const zfp_input* input)
   if (!st->d_u64 && hipMalloc((void**)&st->d_u64, 24) != hipSuccess) return 0;
   if (cached) {  // the caller may have rewritten its buffer since zfp_compress filled the cache: compare every word
     if (!dev_stream) {
-      cached = hash_words((const uint64_t*)s->begin, st->words) == st->hash;
+      cached = st->shadow.size() == st->words &&
+               std::memcmp(s->begin, st->shadow.data(), st->words * sizeof(uint64_t)) == 0;
     } else {
       uint64_t differ = 1;
       if (gcow::launch_words_differ((const uint64_t*)s->begin, (const uint64_t*)st->d_stream, st->words, st->d_u64 + 2,

@@ -2147,15 +2147,13 @@ static hipError_t launch_tiles_t(const FieldDesc& F, const Params& p, const Tile
     return hipGetLastError();
   }
   const bool var1d = D == 1 && T == 256 && p.minbits <= 1 && p.maxbits >= 160;
-  // GCOW_VAR1D_SINGLE_PASS=1 (A/B, tests): the single-pass look-back encoder (var1d.hip). Not the default: on C5 it
-  // ran 0.907 ms against 0.757 ms for count + scan + encode (profiles/r03_c5_single_pass_ab.log)
-  const char* single = getenv("GCOW_VAR1D_SINGLE_PASS");
-  if (var1d && single && single[0] == '1')
-    return launch_encode1d_var_sp(F, p, out32, ws_sums, d_total, index, index_shift, d_base, st);
-  // GCOW_VAR1D_FORM=range (A/B, tests): the count + scan + k_encode1d_var form over ranges of plan.range blocks.
+  // variant 2 (A/B, tests): the single-pass look-back encoder (var1d.hip). Not the default: on C5 it ran 0.907 ms
+  // against 0.757 ms for count + scan + encode (profiles/r03_c5_single_pass_ab.log)
+  const int form = g_var1d_variant.form;
+  if (var1d && form == 2) return launch_encode1d_var_sp(F, p, out32, ws_sums, d_total, index, index_shift, d_base, st);
+  // variant 1 (A/B, tests): the count + scan + k_encode1d_var form over ranges of plan.range blocks.
   // Default: the tile form (var1d.hip: count per tile with byte lengths, scan, the tile coder placed by the scan)
-  const char* form = getenv("GCOW_VAR1D_FORM");
-  if (var1d && !(form && form[0] == 'r'))
+  if (var1d && form != 1)
     return launch_encode1d_var_tile(F, p, out32, ws_sums, d_total, index, index_shift, d_base, st);
   if (var1d) k_count1d_var<DT, 4><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);
   else k_count<D, DT, T><<<plan.nranges, T, 0, st>>>(F, p, plan.range, ws_sums);

@@ -70,6 +70,15 @@ hipError_t launch_scan_ranges(const uint64_t* sums, uint32_t nranges, uint64_t* 
 hipError_t launch_set_u64(uint64_t* p, uint64_t v, void* stream);
 // Single-pass 1-D variable-rate encoder (var1d.hip): minbits <= 1, maxbits >= 160; ws = var1d_sp_workspace_bytes().
 size_t var1d_sp_workspace_bytes(uint64_t nblocks);
+// A/B variants of the 1-D variable-rate encoder, for tests and measurement tools only (set through the C ABI's
+// gcow_debug_set_var1d_variant; the product default is the tile form): form 0 = tile, 1 = range (count + scan +
+// k_encode1d_var), 2 = the look-back single pass; spin = polls before a missing predecessor's total is computed
+// locally (< 0: V1SPIN); stats != 0: the look-back records its statistics in the workspace.
+struct Var1dVariant {
+  int form, spin, stats;
+};
+extern Var1dVariant g_var1d_variant;
+
 hipError_t launch_encode1d_var_sp(const FieldDesc& F, const Params& p, uint32_t* out32, uint64_t* ws,
                                   uint64_t* d_total, uint64_t* index, uint32_t index_shift, const uint64_t* d_base,
                                   void* stream);

@@ -328,7 +328,7 @@ __device__ uint64_t v1_lookback(uint64_t* status, uint32_t t, uint64_t base0, co
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
     excl += x;
     if (incl) {
-      if (stats && lane == 0) {  // GCOW_VAR1D_STATS: look-back behaviour, summed over the launch
+      if (stats && lane == 0) {  // variant stats: look-back behaviour, summed over the launch
         atomicAdd((unsigned long long*)stats, (unsigned long long)polls);
         atomicAdd((unsigned long long*)stats + 1, (unsigned long long)fallbacks);
         atomicAdd((unsigned long long*)stats + 2, (unsigned long long)windows);
@@ -502,6 +502,8 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, 
 }
 
 // The workspace: status[ntiles] then bnd[ntiles] (uint64 each) and 4 words of statistics, zeroed before the launch.
+Var1dVariant g_var1d_variant = {0, -1, 0};
+
 size_t var1d_sp_workspace_bytes(uint64_t nblocks)
 {
   const uint64_t ntiles = (nblocks + V1TILE - 1) / V1TILE;
@@ -518,12 +520,11 @@ hipError_t launch_encode1d_var_sp(const FieldDesc& F, const Params& p, uint32_t*
   if (e != hipSuccess) return e;
   uint64_t* status = ws;
   uint64_t* bnd = ws + ntiles;
-  // GCOW_VAR1D_SPIN (tests): polls before a missing predecessor's total is computed locally; 0 exercises that path
-  const char* ev = getenv("GCOW_VAR1D_SPIN");
-  const uint32_t spin = ev ? (uint32_t)strtoul(ev, nullptr, 10) : V1SPIN;
-  // GCOW_VAR1D_STATS (measurement): polls, fallbacks, look-back windows, polling tiles, most polls, polls of the
-  // first 2048 tiles into ws[2 ntiles .. + 6)
-  uint64_t* stats = getenv("GCOW_VAR1D_STATS") ? ws + 2 * (size_t)ntiles : nullptr;
+  // spin (tests): polls before a missing predecessor's total is computed locally; 0 exercises that path
+  const uint32_t spin = g_var1d_variant.spin >= 0 ? (uint32_t)g_var1d_variant.spin : V1SPIN;
+  // stats (measurement): polls, fallbacks, look-back windows, polling tiles, most polls, polls of the first 2048
+  // tiles into ws[2 ntiles .. + 6)
+  uint64_t* stats = g_var1d_variant.stats ? ws + 2 * (size_t)ntiles : nullptr;
   if (F.dtype == DT_BF16)
     k_encode1d_var_sp<DT_BF16><<<ntiles, V1T, 0, st>>>(F, p, status, bnd, out32, index, index_shift, d_base, d_total,
                                                        ntiles, spin, stats);

@@ -19,6 +19,7 @@ import contextlib
 import queue
 import threading
 from dataclasses import dataclass, field
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -32,19 +33,56 @@ INDEX_STRIDE = 16  # block index spacing the multi-stream decoder reads (one ent
 
 @dataclass
 class GcowHookState:
+    """Hook state, one per DDP model. `timeout_s` bounds every collective of the variable-rate exchange (its own
+    process group, created at the first variable-rate hook call by every member rank): a rank that fails mid-exchange
+    aborts that group, and its peers fail within the timeout instead of hanging in a collective."""
     params: GcowParams = field(default_factory=lambda: _codec.rate(16, 1))
     process_group: object = None
     codec: object = None  # None: gcow_amd.dist.device_codec()
+    timeout_s: float = 300.0
     _worker: object = field(default=None, repr=False)
     _side: dict = field(default_factory=dict, repr=False)
+    _comm_group: object = field(default=None, repr=False)
 
     def get_codec(self):
         return self.codec or gdist.device_codec()
 
     def worker(self) -> "_CommWorker":
         if self._worker is None:
-            self._worker = _CommWorker()
+            self._worker = _CommWorker(self._abort_comm_group)
         return self._worker
+
+    def __post_init__(self):
+        # the exchange group is created here when possible: every rank builds its hook state at the same point of
+        # its setup, in the same order, so group creation needs no care later (creating it inside the hook would
+        # block the autograd thread until every rank reached that bucket)
+        if dist.is_available() and dist.is_initialized() and not _codec.is_fixed(self.params):
+            if dist.get_world_size(self.process_group) > 1:
+                self.comm_group()
+
+    def comm_group(self):
+        """The variable-rate exchange's process group: the hook's ranks, a group of its own so that its collectives
+        (issued from the comm thread) never interleave with collectives DDP issues on `process_group` from the
+        autograd thread (e.g. the find_unused_parameters all-reduce). Created with the state (or, for a state built
+        before init_process_group, by the comm thread's first exchange); only member ranks synchronise
+        (use_local_synchronization)."""
+        if self._comm_group is None:
+            ranks = dist.get_process_group_ranks(self.process_group or dist.group.WORLD)
+            self._comm_group = dist.new_group(ranks=ranks, timeout=timedelta(seconds=self.timeout_s),
+                                              use_local_synchronization=True)
+        return self._comm_group
+
+    def _abort_comm_group(self, ex):
+        g = self._comm_group
+        if g is None:
+            return
+        try:
+            g.abort()  # NCCL: tears down the communicator; peers' pending collectives error out
+        except Exception:  # noqa: BLE001 -- gloo has no abort; destroying closes its connections
+            try:
+                dist.destroy_process_group(g)
+            except Exception:  # noqa: BLE001
+                pass
 
     def side_stream(self, dev):
         if dev not in self._side:
@@ -88,23 +126,42 @@ def roundtrip_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.T
 class _CommWorker:
     """One FIFO thread per hook state for the variable-rate exchange: its host read of the gathered lengths (which
     size the padded all-gather) blocks this thread only, never the autograd thread, and the collectives it issues
-    keep DDP's bucket order on every rank (one queue)."""
+    keep DDP's bucket order on every rank (one queue).
 
-    def __init__(self):
+    Fail fast: the first exception stops the worker. That bucket's future and every future queued or submitted after
+    it fail at once (DDP raises in its wait instead of hanging on a bucket that never runs), and `on_error` aborts the
+    exchange's process group so that peers blocked in a collective with this rank error out too."""
+
+    def __init__(self, on_error=None):
         self.q = queue.Queue()
+        self.failed = None
+        self.on_error = on_error
         self.t = threading.Thread(target=self._loop, name="gcow-comm", daemon=True)
         self.t.start()
+
+    def _stopped(self):
+        return RuntimeError("gcow comm thread stopped after an earlier failure: %r" % (self.failed,))
 
     def _loop(self):
         while True:
             fn, fut = self.q.get()
+            if self.failed is not None:
+                if not fut.done():
+                    fut.set_exception(self._stopped())
+                continue
             try:
                 fn(fut)  # completes fut itself, inside its stream context
             except Exception as ex:  # surfaces in DDP's wait on the hook future
+                self.failed = ex
                 if not fut.done():
                     fut.set_exception(ex)
+                if self.on_error is not None:
+                    self.on_error(ex)
 
     def submit(self, fn, fut):
+        if self.failed is not None:
+            fut.set_exception(self._stopped())
+            return fut
         self.q.put((fn, fut))
         return fut
 
@@ -134,6 +191,10 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
 
         def finish(f):
             f.wait()
+            if gathered.is_cuda:
+                # the callback runs on a pool stream; without this the allocator could hand `gathered` to the next
+                # bucket's torch.zeros on the autograd stream before the decode below has read it
+                gathered.record_stream(torch.cuda.current_stream(gathered.device))
             mean = cdc.decode_mean(gathered, nw, world, n, p)
             flat.copy_(mean.to(flat.dtype))
             return buf
@@ -151,17 +212,22 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
         fut = torch.futures.Future()
 
     def exchange(fut):
+        if side is not None:
+            torch.cuda.set_device(dev)  # this thread's current device: the bucket's, on every LOCAL_RANK
+        cgroup = state.comm_group() if world > 1 else group
         ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
         with ctx:
             if side is not None:
                 side.wait_event(ev)
-            lens, lens_h = gdist.gather_lengths(bits, dev, group)  # host read: this thread waits, autograd does not
+                for t in (words, bits, index):  # read on the side stream: keep them out of the allocator until then
+                    t.record_stream(side)
+            lens, lens_h = gdist.gather_lengths(bits, dev, cgroup)  # host read: this thread waits, autograd does not
             maxw = max(1, max((b + 63) // 64 for b in lens_h))
-            rank = dist.get_rank(group)
-            gathered = gdist.allgather_padded(words, (lens_h[rank] + 63) // 64, maxw, group, pad=2)
+            rank = dist.get_rank(cgroup)
+            gathered = gdist.allgather_padded(words, (lens_h[rank] + 63) // 64, maxw, cgroup, pad=2)
             ni = index.numel()
             idx = torch.empty(world * ni, dtype=torch.int64, device=dev)
-            gdist.allgather_into(idx, index[:ni].contiguous(), group)
+            gdist.allgather_into(idx, index[:ni].contiguous(), cgroup)
             mean = cdc.decode_mean(gathered, maxw, world, n, p, idx, ni, INDEX_STRIDE)
             flat.copy_(mean.to(flat.dtype))
             # completed inside the side-stream context: the future records its event on this stream, so DDP's wait

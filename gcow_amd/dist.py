@@ -17,6 +17,8 @@ protocol code itself runs unchanged over gloo on CPU tensors with an oracle-back
 """
 from __future__ import annotations
 
+from collections import OrderedDict
+
 import torch
 import torch.distributed as dist
 
@@ -25,10 +27,15 @@ from ._ffi import GcowError
 
 class DeviceCodec:
     """The codec calls the exchange needs, on device tensors through libgcow.so. Encoders are cached per
-    (shape, dtype, params, index stride) so a repeated bucket allocates nothing."""
+    (slot, shape, dtype, params, index stride) so a repeated bucket allocates nothing. The cache is an LRU of at most
+    `max_encoders` entries: DDP rebuilds its buckets after the first iteration (new indices and sizes), and the
+    first iteration's encoders must not hold their output / index / workspace buffers for the life of the process.
+    An evicted encoder's buffers live on while a caller still references them; callers that read them on another
+    stream record that stream on them (gcow_amd.ddp does)."""
 
-    def __init__(self):
-        self._enc = {}
+    def __init__(self, max_encoders: int = 64):
+        self._enc = OrderedDict()
+        self.max_encoders = max(1, int(max_encoders))
 
     def encode(self, x: torch.Tensor, params, index_stride: int = 0, slot=None):
         """-> (words int64 tensor, bits int64[1] tensor on x.device, block index or None). Calls with the same shape,
@@ -40,6 +47,10 @@ class DeviceCodec:
         enc = self._enc.get(key)
         if enc is None:
             enc = self._enc[key] = codec.Encoder((x.numel(),), x.dtype, params, x.device, index_stride)
+            while len(self._enc) > self.max_encoders:
+                self._enc.popitem(last=False)
+        else:
+            self._enc.move_to_end(key)
         e = enc(x if x.is_contiguous() else x.contiguous())
         return e.words, e.bits_dev, e.index
 

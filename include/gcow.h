@@ -329,6 +329,13 @@ gcow_status gcow_copy_pattern_device(const void* d_in, int dtype, size_t nvals, 
 gcow_status gcow_fill_normal_device(float* d_out, size_t count, double sigma, uint64_t seed, int inject,
                                     void* hip_stream);
 
+/* TEST / MEASUREMENT ONLY -- not part of the drop-in surface. Selects a measured-and-not-kept form of the 1-D
+ * variable-rate encoder for the whole process (bit-identical output; tests cover each form): form 0 = the tile form
+ * (the default), 1 = count + scan + range coder, 2 = the decoupled look-back single pass; spin (form 2) = polls before
+ * a missing predecessor's total is computed locally (< 0: default); stats != 0 (form 2) records look-back statistics.
+ * No reference counterpart. */
+gcow_status gcow_debug_set_var1d_variant(int form, int spin, int stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,3 +54,27 @@ def test_bench_programmatic_argv_reaches_ranks():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 2
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_fails_loudly_on_oracle_mismatch(n):
+    """a `*_matches_oracle` false in the line (a stitch or shard-offset bug on the driver's N-rank run) must
+    end the run with rc != 0 after the line is printed, not only show up as a boolean in it."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--stub", "--stub-mismatch", "--gpus", str(n), "--steps",
+           "2", "--warmup", "1", "--values", "4096"]
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=e, cwd=ROOT)
+    assert r.returncode != 0
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["stub_check"]["stream_matches_oracle"] is False
+    assert "ORACLE CHECK FAILED" in r.stderr
+
+
+def test_parity_failures_scan():
+    sys.path.insert(0, ROOT)
+    import bench
+    line = {"a": {"gathered_stream_matches_oracle": True}, "c5_sharded": {"stitched_stream_matches_oracle": False},
+            "legs": [{"x_matches_oracle": None}, {"y_matches_oracle": False}]}
+    assert bench.parity_failures(line) == ["c5_sharded.stitched_stream_matches_oracle", "legs.1.y_matches_oracle"]

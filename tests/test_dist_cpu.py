@@ -196,6 +196,52 @@ def _async_hook_worker(rank, world, port, q, mode):
         dist.destroy_process_group()
 
 
+def _fail_fast_worker(rank, world, port, q):
+    _init(rank, world, port)
+    try:
+        import time
+
+        from gcow_amd import ddp
+        from oracle import oracle as O
+        from oracle_codec import OracleCodec
+
+        class Failing(OracleCodec):
+            def decode_mean(self, *a, **k):
+                if rank == 1:
+                    raise RuntimeError("injected codec failure")
+                return super().decode_mean(*a, **k)
+
+        p = _params("acc1e-6")
+        state = ddp.GcowHookState(params=p, codec=Failing(), timeout_s=20.0)
+        g = [torch.from_numpy(O.gen_normal(4 * 500 + 1, 1e-3, 40 + 10 * rank + i, False)) for i in range(2)]
+        t0 = time.perf_counter()
+        futs = [ddp.compressed_allgather_hook(state, _Bucket(g[i], i)) for i in range(2)]
+        errs = []
+        for f in futs:
+            try:
+                f.wait()
+                errs.append(None)
+            except Exception as ex:  # noqa: BLE001
+                errs.append(repr(ex))
+        dt = time.perf_counter() - t0
+        if rank == 1:  # the failing bucket, then the queued one fails at once (its exchange never runs)
+            ok = errs[0] and "injected" in errs[0] and errs[1] and "earlier failure" in errs[1] and dt < 10
+        else:  # bucket 0 completed; bucket 1's collectives fail (the peer aborted the group), well before the timeout
+            ok = errs[0] is None and errs[1] is not None and dt < 15
+        q.put((rank, True if ok else ("rank %d: %s after %.1f s" % (rank, errs, dt))))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_compressed_allgather_hook_fails_fast():
+    """an exception inside one rank's variable-rate exchange (here its decode) must not leave DDP hanging.
+    That rank's bucket future fails with the error, every later bucket's future fails at once, and its exchange
+    group is torn down, so the peer -- blocked in the next bucket's length all-gather -- errors out too."""
+    _run(_fail_fast_worker, 2)
+
+
 @pytest.mark.parametrize("mode", ["rate16", "acc1e-6"])
 def test_compressed_allgather_hook_is_async(mode):
     """The hook returns a pending future before the collective can complete (the other rank joins 1.5 s later) --

@@ -340,6 +340,40 @@ def test_ddp_hooks_world1_bit_exact(gc, orc, nccl_world1, hook, mode):
     assert len(set(seen)) >= 2, seen  # several buckets per step
 
 
+def test_allgather_hook_delayed_decode_stream(gc, orc, nccl_world1):
+    """the fixed-rate hook's decode runs in a Future.then callback on a pool stream; the gathered
+    buffer must stay out of the allocator until that decode has read it. Six equal-size buckets (each a same-size
+    `gathered` request right after the previous bucket's callback returned), and every decode delayed behind a long
+    spin on its stream: every gradient still equals the oracle's decode(encode(local grad)) bit for bit."""
+    from gcow_amd import ddp
+    from gcow_amd.dist import DeviceCodec
+
+    class Delayed(DeviceCodec):
+        def decode_mean(self, *a, **k):
+            torch.cuda._sleep(20_000_000)  # ~10 ms of spinning on the decode's stream before the decode
+            return super().decode_mean(*a, **k)
+
+    params = gc.rate(16, 1)
+    torch.manual_seed(1)
+    layers = lambda: torch.nn.Sequential(*[torch.nn.Linear(640, 640, bias=False) for _ in range(6)]).cuda()  # noqa
+    model, ref = layers(), layers()
+    ref.load_state_dict(model.state_dict())
+    dm = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=1)
+    dm.register_comm_hook(ddp.GcowHookState(params=params, codec=Delayed()), ddp.compressed_allgather_hook)
+    op = orc.expert(*params.tuple())
+    for step in range(2):
+        model.zero_grad()
+        ref.zero_grad()
+        x = torch.randn(32, 640, device="cuda")
+        dm(x).square().mean().backward()
+        ref(x).square().mean().backward()
+        for lm, lr in zip(model, ref):
+            g = lr.weight.grad.reshape(-1).cpu().numpy()
+            want = np.zeros(g.size, np.float32) + orc.decompress(orc.compress(g, op)[0], g.shape, op)
+            got = lm.weight.grad.reshape(-1).cpu().numpy()
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), step
+
+
 # ---------------------------------------------------------------------------------------------- bench N > 1 legs
 def test_bench_multi_legs_world1(gc):
     """bench.py's multi-GPU legs (C4 exchange with the oracle check of the gathered stream, the sub-communicator

@@ -695,17 +695,18 @@ def test_var1d_closed_form_coder(gc, orc, mode):
 
 @pytest.mark.parametrize("env", ["spin0", "single_pass", "range"])
 @pytest.mark.parametrize("mode", ["acc1e-6", "acc1e-3", "prec32", "expert_max", "bf16_acc1e-6"])
-def test_var1d_encoder_forms(gc, orc, env, mode, monkeypatch):
+def test_var1d_encoder_forms(gc, orc, env, mode):
     """The 1-D variable-rate encoder's other forms (the default is a count per 1024-block tile + scan + the tile coder
-    placed by the scan), bit-exact vs the oracle: `single_pass` places the tiles by a decoupled look-back
-    (GCOW_VAR1D_SINGLE_PASS), `spin0` also makes every tile compute a not-yet-published predecessor's total itself
-    (its no-dispatch-order fallback), `range` is count + scan + k_encode1d_var over larger ranges (GCOW_VAR1D_FORM)."""
-    if env == "range":
-        monkeypatch.setenv("GCOW_VAR1D_FORM", "range")
-    else:
-        monkeypatch.setenv("GCOW_VAR1D_SINGLE_PASS", "1")
-    if env == "spin0":
-        monkeypatch.setenv("GCOW_VAR1D_SPIN", "0")
+    placed by the scan), bit-exact vs the oracle: `single_pass` places the tiles by a decoupled look-back, `spin0`
+    also makes every tile compute a not-yet-published predecessor's total itself (its no-dispatch-order fallback),
+    `range` is count + scan + k_encode1d_var over larger ranges (selected through the test-only
+    gcow_debug_set_var1d_variant)."""
+    form = "range" if env == "range" else "single_pass"
+    with gc.var1d_variant(form, spin=0 if env == "spin0" else -1):
+        _var1d_form_case(gc, orc, mode)
+
+
+def _var1d_form_case(gc, orc, mode):
     a = np.concatenate([_adversarial_1d(11), orc.gen_normal((1 << 20) + 3, 1e-3, 78, True)])
     if mode.startswith("bf16"):
         a = (a.view(np.uint32) >> 16).astype(np.uint16)

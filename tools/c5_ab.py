@@ -58,21 +58,15 @@ def main():
         streams = {}
         for rnd in range(2):
             for form in FORMS:
-                os.environ.pop("GCOW_VAR1D_SINGLE_PASS", None)
-                os.environ.pop("GCOW_VAR1D_FORM", None)
-                if form == "single_pass":
-                    os.environ["GCOW_VAR1D_SINGLE_PASS"] = "1"
-                elif form == "range":
-                    os.environ["GCOW_VAR1D_FORM"] = "range"
-                cold, per = timed(lambda: enc(x), 5, 20)
-                st = steady(lambda: enc(x))
-                e = enc(x)
-                bits = e.bits
+                with codec.var1d_variant(form):
+                    cold, per = timed(lambda: enc(x), 5, 20)
+                    st = steady(lambda: enc(x))
+                    e = enc(x)
+                    bits = e.bits
                 if form == "single_pass" and rnd == 0:  # look-back behaviour of one launch
-                    os.environ["GCOW_VAR1D_STATS"] = "1"
-                    enc(x)
-                    torch.cuda.synchronize()
-                    os.environ.pop("GCOW_VAR1D_STATS")
+                    with codec.var1d_variant(form, stats=True):
+                        enc(x)
+                        torch.cuda.synchronize()
                     nt = (n // 4 + 1023) // 1024
                     st_ = enc.ws[2 * nt:2 * nt + 6].tolist()
                     res["lookback"] = {"tiles": nt, "polls": st_[0], "fallbacks": st_[1], "windows": st_[2],
@@ -81,8 +75,6 @@ def main():
                     streams[form] = (bits, e.stream().clone())
                 res.setdefault(form, []).append({"cold_ms": round(cold, 4), "first_ms": round(per[0], 4),
                                                  "steady_ms": round(st, 4)})
-        os.environ.pop("GCOW_VAR1D_SINGLE_PASS", None)
-        os.environ.pop("GCOW_VAR1D_FORM", None)
         s0 = streams[FORMS[0]]
         res["bits_per_value"] = round(s0[0] / n, 3)
         res["streams_equal"] = all(s0[0] == streams[f][0] and torch.equal(s0[1], streams[f][1]) for f in FORMS[1:])

@@ -111,7 +111,10 @@ if __name__ == "__main__":
     ap.add_argument("cases", nargs="*", default=["c3", "c5"])
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--lib", default=None, help="libgcow.so to load instead of the in-tree build")
+    ap.add_argument("--var1d-form", default="tile", choices=sorted(codec.VAR1D_FORMS),
+                    help="1-D variable-rate encoder form (test-only variant setter)")
     a = ap.parse_args()
-    for c in a.cases:
-        globals()[c](a.reps)
+    with codec.var1d_variant(a.var1d_form):
+        for c in a.cases:
+            globals()[c](a.reps)
     print("prof_cases done", flush=True)

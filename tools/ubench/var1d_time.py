@@ -8,14 +8,14 @@ import time
 
 import torch
 
-if "--sp" in sys.argv:
-    os.environ["GCOW_VAR1D_SINGLE_PASS"] = "1"  # the look-back form (else the default tile form)
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 if "--lib" in sys.argv:
     from gcow_amd import _ffi  # noqa: E402
     _ffi.LIB_PATH = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
 from gcow_amd import codec  # noqa: E402
+
+FORM = "single_pass" if "--sp" in sys.argv else "tile"  # --sp: the look-back form (else the default tile form)
 
 
 def timed(fn, warm, steps):
@@ -40,18 +40,18 @@ del x32
 out = {"lib": os.path.basename(sys.argv[sys.argv.index("--lib") + 1]) if "--lib" in sys.argv else "product"}
 for tol in (1e-6, 1e-3):
     enc = codec.Encoder((n,), torch.bfloat16, codec.accuracy(tol), "cuda", index_stride=16)
-    cold = timed(lambda: enc(xb), 5, 20)
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < 0.25:
-        for _ in range(20):
-            enc(xb)
-        torch.cuda.synchronize()
-    d = {"cold_ms": round(cold, 4), "steady_ms": round(timed(lambda: enc(xb), 0, 100), 4)}
+    with codec.var1d_variant(FORM):
+        cold = timed(lambda: enc(xb), 5, 20)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.25:
+            for _ in range(20):
+                enc(xb)
+            torch.cuda.synchronize()
+        d = {"cold_ms": round(cold, 4), "steady_ms": round(timed(lambda: enc(xb), 0, 100), 4)}
     if "--sp" in sys.argv:
-        os.environ["GCOW_VAR1D_STATS"] = "1"  # look-back polls / fallbacks / windows of one launch
-        enc(xb)
-        torch.cuda.synchronize()
-        os.environ.pop("GCOW_VAR1D_STATS")
+        with codec.var1d_variant(FORM, stats=True):  # look-back polls / fallbacks / windows of one launch
+            enc(xb)
+            torch.cuda.synchronize()
         nt = (n // 4 + 1023) // 1024
         d["lookback_polls_fallbacks_windows_polling_max_first2048"] = enc.ws[2 * nt:2 * nt + 6].tolist()
     out["acc%g" % tol] = d
