@@ -52,6 +52,36 @@ __device__ __forceinline__ uint32_t ffbh_u32(uint32_t x)
 
 __device__ __forceinline__ uint64_t lowmask64(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
 
+// ------------------------------------------------------------------------------------------------ LDS staging
+// Workgroup prologues (lookup tables, a stream span) copied global -> LDS with every load issued before the first LDS
+// write: one memory round trip per prologue. The plain `for (j = tid; j < n; j += T) lds[j] = g[j]` has a trip count
+// the compiler cannot see, and compiles to load -> s_waitcnt vmcnt(0) -> ds_write per iteration: one full memory
+// latency per iteration (10-20 of them per workgroup in the decoders before this was changed).
+typedef unsigned int st_v4u __attribute__((ext_vector_type(4)));
+
+// nbytes (<= MAXC * 16) bytes from src (16-byte aligned) to dst[0 .. MAXC) as 16-byte chunks; chunks past nbytes read
+// zero (buffer range check), so every lane issues the same loads. T threads.
+template <uint32_t T, uint32_t MAXC>
+__device__ __forceinline__ void stage_lds16(void* dst, const void* src, uint32_t nbytes)
+{
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(src), 0, (int)nbytes, 0x00020000);
+  constexpr uint32_t R = (MAXC + T - 1) / T;
+  st_v4u v[R];
+#pragma unroll
+  for (uint32_t i = 0; i < R; i++) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((threadIdx.x + T * i) * 16u), 0, 0);
+#pragma unroll
+  for (uint32_t i = 0; i < R; i++)
+    if (MAXC % T == 0 || threadIdx.x + T * i < MAXC) ((st_v4u*)dst)[threadIdx.x + T * i] = v[i];
+}
+
+// A constant table of N 32-bit words (N * 4 a multiple of 16) into LDS.
+template <uint32_t T, uint32_t N>
+__device__ __forceinline__ void stage_table(uint32_t* dst, const void* tab)
+{
+  static_assert(N % 4 == 0, "whole 16-byte chunks");
+  stage_lds16<T, N / 4>(dst, tab, N * 4u);
+}
+
 // ------------------------------------------------------------------------------------------------ stages
 // get_block_exponent + get_scaler_exponent (encode.c:128-152) on bit patterns.
 template <int B>
@@ -498,7 +528,7 @@ __device__ __forceinline__ uint32_t encode_ints(W& w, const uint32_t* u, uint32_
 // appends: n + 1 verbatim/flag bits, and E(r) (hb + m + 1 bits with m = popcount(r), or hb + m - 1 at coefficient
 // 63) built from a 256-entry table of E over 8-bit chunks. Lanes do a fixed amount of work per plane; only chunks
 // past the wave's largest hb are skipped.
-struct DupTab {
+struct alignas(16) DupTab {
   uint32_t v[256];
 };
 

@@ -227,30 +227,31 @@ __global__ __launch_bounds__(64) void k_decode_staged(FieldDesc F, Params p, con
 {
   constexpr int B = Dim<D>::B;
   constexpr uint32_t CAPW = 64 * 1024 / 32;  // 32-bit words
-  __shared__ uint32_t sw[CAPW + 4];
+  __shared__ __attribute__((aligned(16))) uint32_t sw[CAPW + 8];
   const uint32_t tid = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * 64, nb = F.nblocks;
   auto start_of = [&](uint64_t b) { return base_bits + (fixed ? b * p.maxbits : index[b]); };
+  const uint64_t b = b0 + tid;
+  const uint64_t mine = b < nb ? start_of(b) : 0ull;  // requested with the span, not after it
   const uint64_t s0 = start_of(b0);
-  const uint64_t w0 = s0 >> 5;  // 32-bit word index
+  const uint64_t w0 = (s0 >> 5) & ~3ull;  // 32-bit word index, 16-byte aligned
   const uint64_t in_w32 = 2 * in_words;
   const uint64_t wend = b0 + 64 < nb ? (start_of(b0 + 64) + 31) >> 5 : in_w32;
   const uint64_t span = min<uint64_t>(wend, in_w32) - w0;
   const bool staged = span <= CAPW;
   const uint32_t* in32 = (const uint32_t*)in;
-  if (staged)
-    for (uint32_t j = tid; j < (uint32_t)span + 4; j += 64) sw[j] = w0 + j < in_w32 ? in32[w0 + j] : 0u;
+  // the span (zeros after it: the reader looks up to 3 words past a block's last bit) in one memory round trip
+  if (staged) stage_lds16<64, (CAPW + 8) / 4>(sw, in32 + w0, (uint32_t)(4 * span));
   __syncthreads();
-  const uint64_t b = b0 + tid;
   if (b >= nb) return;
   float f[B];
   uint64_t end;
   if (staged) {
-    WordBitReader r{sw, (uint32_t)(start_of(b) - 32 * w0)};
+    WordBitReader r{sw, (uint32_t)(mine - 32 * w0)};
     decode_block<D>(r, p, f);
     end = r.pos + 32 * w0;
   } else {
-    BitReader r{in, start_of(b)};
+    BitReader r{in, mine};
     decode_block<D>(r, p, f);
     end = r.pos;
   }

@@ -365,6 +365,13 @@ __device__ __forceinline__ uint32_t buf_load_u32(uint32_t off, pipe_v4i rs)
   return v;
 }
 
+__device__ __forceinline__ pipe_v4u buf_load_b128(uint32_t off, pipe_v4i rs)
+{
+  pipe_v4u v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+  return v;
+}
+
 template <int DT, uint32_t WB, int U, uint32_t T = 256, int V = 0>
 __global__ __launch_bounds__(T) void k_encode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
                                                          void* __restrict__ out)
@@ -789,13 +796,14 @@ __global__ __launch_bounds__(256) void k_encode1d_var(FieldDesc F, Params p, uin
   __shared__ uint64_t lds64[(31 + T * U * 160 + 63) / 64 + 4];
   __shared__ uint32_t scan_sh[T / 64];
   __shared__ uint16_t tab[80];
-  __shared__ uint32_t tab2[1280];
+  __shared__ __attribute__((aligned(16))) uint32_t tab2[1280];
   __shared__ uint32_t rs[1024];  // window spread tables (window_lds)
   uint32_t* lds = (uint32_t*)lds64;
   const uint32_t tid = threadIdx.x;
   if (tid < 80) tab[tid] = plane_entry4(tid);
-  for (uint32_t t = tid; t < 1280; t += T) tab2[t] = g_plane_tab5.v[t];
-  for (uint32_t t = tid; t < 1024; t += T) rs[t] = rspread_entry(t);
+  stage_table<T, 1280>(tab2, g_plane_tab5.v);
+#pragma unroll
+  for (uint32_t t = 0; t < 1024 / T; t++) rs[tid + T * t] = rspread_entry(tid + T * t);
   const uint64_t b0 = (uint64_t)blockIdx.x * range;
   const uint64_t b1 = min<uint64_t>(b0 + range, F.nblocks);
   const bool final_range = b1 == F.nblocks;
@@ -1240,7 +1248,7 @@ __global__ void k_widen_u32(const uint32_t* __restrict__ a, uint32_t n, uint64_t
 // Entry (n, r, b): decode one plane from state n with the next 7 stream bits b of which only r + 1 are inside the
 // block's bit budget (r = 7: at least 8). The budget matters exactly like libzfp's: when it runs out inside the
 // unary scan, decode_ints still deposits the coefficient at the current n (x += 1 << n++ after the inner loop).
-struct DecTab1 {
+struct alignas(16) DecTab1 {
   uint16_t v[5 * 8 * 128];
 };
 
@@ -1278,6 +1286,21 @@ __host__ __device__ constexpr DecTab1 make_dec_tab1()
 }
 
 __device__ const DecTab1 g_dec_tab1 = make_dec_tab1();
+
+// The no-budget rows (r = 7) of the plane table, indexed (n, 7 bits): what the variable-rate decoders use (640 entries,
+// 1280 bytes: one 16-byte load for 80 lanes).
+struct alignas(16) DecTab7 {
+  uint16_t v[5 * 128];
+};
+
+__host__ __device__ constexpr DecTab7 make_dec_tab7()
+{
+  DecTab7 T{};
+  for (uint32_t t = 0; t < 5 * 128; t++) T.v[t] = (uint16_t)dec_plane_cx(((((t >> 7) << 3) | 7u) << 7) | (t & 127u));
+  return T;
+}
+
+__device__ const DecTab7 g_dec_tab7 = make_dec_tab7();
 
 __device__ __forceinline__ uint64_t inv_transpose4x16(uint64_t x)
 {
@@ -1368,16 +1391,27 @@ template <uint32_t WB, int U>
 __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
                                                            float* __restrict__ out, uint64_t base_bits)
 {
-  __shared__ uint16_t dtab[5 * 8 * 128];
+  __shared__ __attribute__((aligned(16))) uint16_t dtab[5 * 8 * 128];
   constexpr uint32_t WBYTES = WB / 8;
   const pipe_v4i rin = buf_rsrc((const char*)in + base_bits / 8, nfull * WBYTES);
   const __amdgpu_buffer_rsrc_t rout_b = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(nfull * 16u), 0x00020000);
   const uint32_t b0 = blockIdx.x * (256u * U) + threadIdx.x;
+  // the 10 KiB plane table (640 16-byte chunks, 3 per lane; the range check zeroes the rest) is requested first and
+  // waited for with vmcnt(U): the U word loads behind it stay in flight, and no wait counts a memory round trip per
+  // table chunk (as a compiler-issued copy loop does)
+  constexpr uint32_t TCH = sizeof(DecTab1) / 16, TR = (TCH + 255) / 256;
+  const pipe_v4i rt = buf_rsrc(&g_dec_tab1, sizeof(DecTab1));
+  pipe_v4u tv[TR];
+#pragma unroll
+  for (uint32_t i = 0; i < TR; i++) tv[i] = buf_load_b128((threadIdx.x + 256u * i) * 16u, rt);
   typename PipeWord<WB>::T r[U];
 #pragma unroll
   for (int k = 0; k < U; k++) r[k] = PipeWord<WB>::load((b0 + 256u * k) * WBYTES, rin);
-  for (uint32_t t = threadIdx.x; t < 5 * 8 * 128 / 2; t += 256)  // 10 KiB, copied as dwords
-    ((uint32_t*)dtab)[t] = ((const uint32_t*)g_dec_tab1.v)[t];
+  static_assert(TR == 3, "the wait below ties three table registers");
+  asm volatile("s_waitcnt vmcnt(%3)" : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]) : "n"(U) : "memory");
+#pragma unroll
+  for (uint32_t i = 0; i < TR; i++)
+    if (threadIdx.x + 256u * i < TCH) ((pipe_v4u*)dtab)[threadIdx.x + 256u * i] = tv[i];
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < U; k++) {
@@ -1508,8 +1542,8 @@ __global__ __launch_bounds__(256) void k_decode1d_var(FieldDesc F, Params p, con
                                                       uint64_t nchunks, uint64_t base_bits,
                                                       uint64_t* __restrict__ end_out)
 {
-  __shared__ uint16_t dtab[5 * 128];  // r = 7 rows of the plane table
-  for (uint32_t t = threadIdx.x; t < 5 * 128; t += 256) dtab[t] = g_dec_tab1.v[(((t >> 7) << 3) | 7u) << 7 | (t & 127u)];
+  __shared__ __attribute__((aligned(16))) uint16_t dtab[5 * 128];  // r = 7 rows of the plane table
+  stage_lds16<256, sizeof(DecTab7) / 16>(dtab, &g_dec_tab7, sizeof(DecTab7));
   __syncthreads();
   const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (c >= nchunks) return;
@@ -1547,24 +1581,25 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_staged(FieldDesc F, Para
                                                                uint64_t nchunks, uint64_t base_bits,
                                                                uint64_t* __restrict__ end_out)
 {
-  constexpr uint32_t CAP = LANES * 16 * 80 / 64;
-  __shared__ uint16_t dt7[5 * 128];
-  __shared__ uint64_t sw[CAP + 2];
+  constexpr uint32_t CAP = LANES * 16 * 80 / 64;  // stream words the stage holds
+  __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
+  __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
   const uint32_t tid = threadIdx.x;
-  for (uint32_t t = tid; t < 5 * 128; t += LANES) dt7[t] = g_dec_tab1.v[(((t >> 7) << 3) | 7u) << 7 | (t & 127u)];
   const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
-  const uint64_t w0 = (base_bits + index[c0]) >> 6;
+  const uint64_t w0 = ((base_bits + index[c0]) >> 6) & ~1ull;  // 16-byte aligned start
   const uint64_t wend = c0 + LANES < nchunks ? ((base_bits + index[c0 + LANES] + 63) >> 6) : in_words;
   const uint64_t span = min<uint64_t>(wend, in_words) - w0;
   const bool staged = span <= CAP;
-  if (staged)
-    for (uint32_t j = tid; j < (uint32_t)span + 2; j += LANES) sw[j] = w0 + j < in_words ? in[w0 + j] : 0ull;
-  __syncthreads();
   const uint64_t c = c0 + tid;
+  const uint64_t mine = c < nchunks ? index[c] : 0ull;  // requested with the span, not after it
+  stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
+  // the span (and zeros after it: the windows read up to two words past a block's last bit) in one round trip
+  if (staged) stage_lds16<LANES, (CAP + 4) / 2>(sw, in + w0, (uint32_t)(8 * span));
+  __syncthreads();
   if (c >= nchunks) return;
   const uint64_t b0 = c * 16, b1 = min<uint64_t>(b0 + 16, F.nblocks);
   float* out = (float*)F.data;
-  uint64_t pos = base_bits + index[c];
+  uint64_t pos = base_bits + mine;
   auto run = [&](const auto& win, uint64_t rel) {
     pos -= rel;
     if (4 * b1 <= F.n[0] && b1 - b0 == 16) {
@@ -1809,9 +1844,9 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d(FieldDesc F, Params
                                                              uint64_t stream_words, uint32_t nstreams)
 {
 #pragma clang fp contract(off)
-  __shared__ uint16_t dtab[WB ? 5 * 8 * 128 : 1];
+  __shared__ __attribute__((aligned(16))) uint16_t dtab[WB ? 5 * 8 * 128 : 8];
   if (WB) {
-    for (uint32_t t = threadIdx.x; t < 5 * 8 * 128 / 2; t += 256) ((uint32_t*)dtab)[t] = ((const uint32_t*)g_dec_tab1.v)[t];
+    stage_lds16<256, sizeof(DecTab1) / 16>(dtab, &g_dec_tab1, sizeof(DecTab1));
     __syncthreads();
   }
   const uint64_t b = (uint64_t)blockIdx.x * 256u + threadIdx.x;
@@ -1846,10 +1881,10 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
 {
 #pragma clang fp contract(off)
   constexpr uint32_t CAP = LANES * 16 * 80 / 64;
-  __shared__ uint16_t dt7[5 * 128];
-  __shared__ uint64_t sw[CAP + 2];
+  __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
+  __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
   const uint32_t tid = threadIdx.x;
-  for (uint32_t t = tid; t < 5 * 128; t += LANES) dt7[t] = g_dec_tab1.v[(((t >> 7) << 3) | 7u) << 7 | (t & 127u)];
+  stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
   const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
   const uint64_t c = c0 + tid;
   const uint64_t b0 = c * 16, b1 = min<uint64_t>(b0 + 16, F.nblocks);
@@ -1859,13 +1894,15 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
   for (uint32_t r = 0; r < nstreams; r++) {
     const uint64_t* sr = in + (uint64_t)r * stream_words;
     const uint64_t* ix = index + (uint64_t)r * index_words;
-    const uint64_t w0 = ix[c0] >> 6;
+    // the staged span starts on a 16-byte boundary of the whole buffer (streams are stream_words apart, which may be
+    // odd): w0 may be one word before this stream's first word (the previous stream's last word, never decoded)
+    const uint64_t sbase = (uint64_t)r * stream_words;
+    const int64_t w0 = (int64_t)((sbase + (ix[c0] >> 6)) & ~1ull) - (int64_t)sbase;
     const uint64_t wend = c0 + LANES < nchunks ? ((ix[c0 + LANES] + 63) >> 6) : stream_words;
-    const uint64_t span = min<uint64_t>(wend, stream_words) - w0;
+    const uint64_t span = (uint64_t)((int64_t)min<uint64_t>(wend, stream_words) - w0);
     const bool staged = span <= CAP;
     __syncthreads();  // the previous stream's span is no longer read
-    if (staged)
-      for (uint32_t j = tid; j < (uint32_t)span + 2; j += LANES) sw[j] = w0 + j < stream_words ? sr[w0 + j] : 0ull;
+    if (staged) stage_lds16<LANES, (CAP + 4) / 2>(sw, sr + w0, (uint32_t)(8 * span));
     __syncthreads();
     if (c >= nchunks) continue;
     uint64_t pos = ix[c];
@@ -1881,7 +1918,7 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
       }
     };
     if (staged) {
-      pos -= 64 * w0;
+      pos = (uint64_t)((int64_t)pos - 64 * w0);
       run(LdsWindow{sw});
     } else {
       run(GlobalWindow{sr});

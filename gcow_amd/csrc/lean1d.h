@@ -35,7 +35,7 @@ __device__ __forceinline__ uint16_t plane_entry4(uint32_t t)
 }
 
 // Compile-time plane-pair table (two plane codes per entry), copied to LDS by each workgroup.
-struct PlaneTab2 {
+struct alignas(16) PlaneTab2 {
   uint32_t v[1280];
 };
 

@@ -73,10 +73,10 @@ __global__ __launch_bounds__(T) void k_encode_tiles(FieldDesc F, Params p, uint3
   constexpr int B = Dim<D>::B;
   extern __shared__ uint32_t lds[];
   __shared__ uint32_t scan_sh[T / 64 > 0 ? T / 64 : 1];
-  __shared__ uint32_t dup[B == 64 ? 256 : 1];  // E table of the 64-coefficient plane coder
+  __shared__ __attribute__((aligned(16))) uint32_t dup[B == 64 ? 256 : 4];  // E table of the 64-coefficient plane coder
   const uint32_t tid = threadIdx.x;
   if constexpr (B == 64) {
-    for (uint32_t t = tid; t < 256; t += T) dup[t] = g_dup_tab.v[t];
+    stage_table<T, 256>(dup, g_dup_tab.v);
     __syncthreads();
   }
   const uint64_t b0 = (uint64_t)blockIdx.x * range;

@@ -358,7 +358,7 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, 
                                                          uint64_t* __restrict__ d_total, uint32_t ntiles,
                                                          uint32_t spin, uint64_t* __restrict__ stats)
 {
-  __shared__ uint32_t tab[1280];  // pair table (lean-5 entries, rows n >= 3 empty)
+  __shared__ __attribute__((aligned(16))) uint32_t tab[1280];  // pair table (lean-5 entries, rows n >= 3 empty)
   __shared__ uint32_t rs[1024];   // window spread tables
   __shared__ uint64_t win[V1Q];   // the tile's code, tile-relative bit positions
   __shared__ uint32_t scan_sh[V1T / 64];
@@ -367,8 +367,9 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_sp(FieldDesc F, Params p, 
   uint32_t* win32 = (uint32_t*)win;
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t t = blockIdx.x;
-  for (uint32_t i = tid; i < 1280; i += V1T) tab[i] = g_plane_tab_var.v[i];
-  for (uint32_t i = tid; i < 1024; i += V1T) rs[i] = rspread_entry(i);
+  stage_table<V1T, 1280>(tab, g_plane_tab_var.v);
+#pragma unroll
+  for (uint32_t i = 0; i < 1024 / V1T; i++) rs[tid + V1T * i] = rspread_entry(tid + V1T * i);
   if (tid == 0) s_special = 0;
   const bool wide_ok = F.vec && (((uintptr_t)F.data) & 15u) == 0;
   const uint64_t base0 = d_base ? *d_base : 0ull;
@@ -895,21 +896,28 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_tile(FieldDesc F, Params p
                                                            uint32_t index_shift, uint32_t ntiles,
                                                            uint32_t* __restrict__ over)
 {
-  __shared__ uint32_t tab[V1TAB];  // pair table rows 0..3 (lean-5 entries, row 3 empty)
+  __shared__ __attribute__((aligned(16))) uint32_t tab[V1TAB];  // pair table rows 0..3 (lean-5 entries, row 3 empty)
   __shared__ uint32_t rs[1024];    // window spread tables
   __shared__ __attribute__((aligned(16))) uint64_t win[V1QS];  // the tile's code from bit base & 127 of its window
   __shared__ uint32_t scan_sh[V1T / 64];
   __shared__ uint32_t s_special;
   const uint32_t t = blockIdx.x;
+  // every load the tile needs is issued before anything waits (one memory round trip per workgroup): the input rows,
+  // the lane's byte lengths, the pair table, the tile's stream offsets
+  V1Raw<DT> raw;
+  raw.load(F, t, F.vec && (((uintptr_t)F.data) & 15u) == 0);
+  const uint32_t lw = lens8[(size_t)t * V1T + threadIdx.x];
+  stage_table<V1T, V1TAB>(tab, g_plane_tab_var.v);
+#pragma unroll
+  for (uint32_t i = 0; i < 1024 / V1T; i++) rs[threadIdx.x + V1T * i] = rspread_entry(threadIdx.x + V1T * i);
   const uint64_t B = rbase[t];
   const uint32_t total = (uint32_t)(rbase[t + 1] - B);
   if (v1_tile_qwords(B, total) > V1QS) {  // oversized: listed for k_encode1d_var_tile_big (over[0] = count)
     if (threadIdx.x == 0) over[1 + atomicAdd(over, 1u)] = t;
     return;
   }
-  for (uint32_t i = threadIdx.x; i < V1TAB; i += V1T) tab[i] = g_plane_tab_var.v[i];
-  for (uint32_t i = threadIdx.x; i < 1024; i += V1T) rs[i] = rspread_entry(i);
-  v1_tile<DT>(F, p, t, B, total, lens8, out32, index, index_shift, ntiles, tab, rs, win, scan_sh, &s_special);
+  v1_tile_code<DT>(F, p, t, B, raw, lw, index, index_shift, tab, rs, win, scan_sh, &s_special);
+  v1_tile_store(t, B, total, win, out32, ntiles);
 }
 
 template <int DT>
@@ -920,15 +928,16 @@ __global__ __launch_bounds__(V1T) void k_encode1d_var_tile_big(FieldDesc F, Para
                                                                uint64_t* __restrict__ index, uint32_t index_shift,
                                                                uint32_t ntiles, const uint32_t* __restrict__ over)
 {
-  __shared__ uint32_t tab[V1TAB];
+  __shared__ __attribute__((aligned(16))) uint32_t tab[V1TAB];
   __shared__ uint32_t rs[1024];
   __shared__ __attribute__((aligned(16))) uint64_t win[V1Q + 2];
   __shared__ uint32_t scan_sh[V1T / 64];
   __shared__ uint32_t s_special;
   const uint32_t n = over[0];
   if (blockIdx.x >= n) return;
-  for (uint32_t i = threadIdx.x; i < V1TAB; i += V1T) tab[i] = g_plane_tab_var.v[i];
-  for (uint32_t i = threadIdx.x; i < 1024; i += V1T) rs[i] = rspread_entry(i);
+  stage_table<V1T, V1TAB>(tab, g_plane_tab_var.v);
+#pragma unroll
+  for (uint32_t i = 0; i < 1024 / V1T; i++) rs[threadIdx.x + V1T * i] = rspread_entry(threadIdx.x + V1T * i);
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t t = over[1 + i];
     const uint64_t B = rbase[t];
