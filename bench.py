@@ -467,14 +467,85 @@ def leg_configs(ctx):
         # twice (count + coder) and the byte lengths written and read once
         er["traffic"], src = load_pmc_traffic("k_count1d_var_tile", name + "_256Mi")
         er["traffic_source"] = src
+        # the receive side (the caller's codec cost is compress + decompress, hw/models/train_imagenet.py:458-467):
+        # the 1-D variable-rate decode of this stream (block index every 16 blocks) into fp32
+        e = enc(xb, st)
+        back = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+        _, dper = timed(ctx, lambda: codec.decode(e, out=back, stream=st), 5, 20, stream=st)
+        dk = sum(dper) / len(dper)
+        dr = roof(cbits / 8, n * 4, dk, "k_decode1d_var_lean<128>", basis="write")
         out[name] = {"encode_ms": round(k_ms, 4), "encode_GiBps_input": round(gib(n * 2, k_ms), 2),
                      "bits_per_value": round(cbits / n, 3), "encode_roofline": er,
+                     "decode_ms": round(dk, 4), "decode_GiBps_output": round(gib(n * 4, dk), 2),
+                     "decode_roofline": dr,
                      "host_path_ms": round(h_ms, 3), "host_path_GiBps_input": round(gib(n * 2, h_ms), 2),
                      "host_path_note": "pinned bf16 H2D + encode + D2H of the stream, 8 overlapped chunks (PCIe-bound)"}
-        del enc, h_in, h_out, henc
+        del enc, h_in, h_out, henc, e, back
     del xb
     torch.cuda.empty_cache()
+    # the same bucket in fp32 at the caller's default tolerance: encode and the receive-side decode
+    x32 = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+    codec.fill_normal(x32, 1e-3, seed=SEED, inject=True)
+    p = codec.accuracy(1e-6)
+    enc = codec.Encoder((n,), torch.float32, p, ctx.dev, index_stride=16)
+    st = torch.cuda.current_stream(ctx.dev)
+    _, per = timed(ctx, lambda: enc(x32, st), 5, 20, stream=st)
+    k_ms = sum(per) / len(per)
+    e = enc(x32, st)
+    cbits = e.bits
+    back = torch.empty_like(x32)
+    _, dper = timed(ctx, lambda: codec.decode(e, out=back, stream=st), 5, 20, stream=st)
+    dk = sum(dper) / len(dper)
+    out["var1d_f32_acc1e-6"] = {
+        "encode_ms": round(k_ms, 4), "encode_GiBps_input": round(gib(n * 4, k_ms), 2),
+        "bits_per_value": round(cbits / n, 3),
+        "encode_roofline": roof(n * 4, cbits / 8, k_ms, "k_count1d_var_tile + k_scan_ranges_mw + k_encode1d_var_tile"),
+        "decode_ms": round(dk, 4), "decode_GiBps_output": round(gib(n * 4, dk), 2),
+        "decode_roofline": roof(cbits / 8, n * 4, dk, "k_decode1d_var_lean<128>", basis="write")}
+    del x32, enc, e, back
+    torch.cuda.empty_cache()
+    out["decode_mean_w8"] = leg_decode_mean(ctx)
     return out
+
+
+def leg_decode_mean(ctx, W: int = 8):
+    """The receive side of gcow_amd.ddp.compressed_allgather_hook on one GPU: W = 8 ranks' streams of 256 Mi fp32
+    values (W different buckets of the bench distribution) decoded and averaged in one launch (codec.decode_mean), at
+    rate 16 (the caller's default rate, hw/models/train_imagenet.py:155) and accuracy 1e-6 (the caller's default
+    tolerance, :154). Roofline basis: the fp32 mean written; read + write adds the W compressed streams."""
+    from gcow_amd import codec
+    n = N_VALUES
+    x = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+    mean = torch.empty_like(x)
+    st = torch.cuda.current_stream(ctx.dev)
+    res = {}
+    for name, p, stride in (("rate16", codec.rate(16, 1), 0), ("acc1e-6", codec.accuracy(1e-6), 16)):
+        enc = codec.Encoder((n,), torch.float32, p, ctx.dev, index_stride=stride)
+        parts, idx, bits = [], [], 0
+        for r in range(W):
+            codec.fill_normal(x, 1e-3, seed=SEED + r, inject=True)
+            e = enc(x, st)
+            parts.append(e.stream().clone())
+            if stride:
+                idx.append(e.index.clone())
+            bits += e.bits
+        sw = max(t.numel() for t in parts)
+        buf = torch.zeros(W * sw + 2, dtype=torch.int64, device=ctx.dev)
+        for r, t in enumerate(parts):
+            buf[r * sw:r * sw + t.numel()] = t
+        ix = torch.cat(idx) if stride else None
+        ni = idx[0].numel() if stride else 0
+        del parts, idx, enc
+        _, per = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ix, ni, stride, out=mean, stream=st), 3, 10,
+                       stream=st)
+        k = sum(per) / len(per)
+        kname = "k_decode_mean_fixed1d<64>" if stride == 0 else "k_decode_mean1d_var<128>"
+        res[name] = {"streams": W, "values": n, "kernel_ms": round(k, 4), "bits_per_value": round(bits / W / n, 3),
+                     "roofline": roof(bits / 8, n * 4, k, kname, basis="write")}
+        del buf, ix
+        torch.cuda.empty_cache()
+    del x, mean
+    return res
 
 
 def _cpu_model() -> str:

@@ -1622,6 +1622,195 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_staged(FieldDesc F, Para
   if (end_out && c == nchunks - 1) *end_out = pos;
 }
 
+// ------------------------------------------------------------------------------------------------ lean 1-D var decode
+// The variable-rate block decoder of the staged kernels, cut to what a block needs (libzfp decode_ints semantics,
+// decode.c:141-183 with the block-size fix; minbits <= 1, maxbits >= 160, so no budget truncates):
+//  * one 64-bit window at the block start gives the header, the precision and the run of empty planes (ctz over the
+//    55 bits after the header covers any np <= 32) and, in the common case, the group phase's bits too (the window
+//    is re-read only when a group plane's 7 lookup bits would run past it);
+//  * the group phase (planes while fewer than 3 coefficients are significant) is at most 8 planes here, its nibbles
+//    packed into one 32-bit word; a block whose group phase is longer takes the general decoder (rare: three
+//    coefficients spread over more than 8 planes);
+//  * the verbatim nibble run (4 bits per remaining plane) is one window, two past 64 bits;
+//  * the inverse 4 x 16 bit transposes run for the planes present: the second half only when more than 16 planes
+//    are coded (accuracy 1e-6 on gradient-scale data codes ~14).
+// Positions are 32-bit, relative to the staged words (LDS), and windows are built from three 32-bit words with two
+// v_alignbit_b32.
+__device__ __forceinline__ uint64_t lds_win64(const uint32_t* w, uint32_t pos)
+{
+  const uint32_t i = pos >> 5;
+  const uint32_t a = w[i], b = w[i + 1], c = w[i + 2];
+  return ((uint64_t)__builtin_amdgcn_alignbit(c, b, pos) << 32) | __builtin_amdgcn_alignbit(b, a, pos);
+}
+
+// returns false when the block needs the general decoder (pos unchanged then)
+__device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& pos, const uint16_t* dt7, int cexp,
+                                                 int maxprec, float* f)
+{
+  const uint64_t w = lds_win64(sw, pos);
+  const int emax = (int)((w >> 1) & 255u) - 127;
+  const int np = min(32, min(maxprec, max(0, emax + cexp)));  // coded planes 31 .. 32 - np
+  const uint64_t r = w >> 9;
+  const int z = r ? (int)__builtin_ctzll(r) : 64;  // empty planes (any np <= 32 < 55 is covered)
+  f[0] = f[1] = f[2] = f[3] = 0.0f;
+  if (!(w & 1u)) {  // zero block (or no precision): one 0 bit
+    pos += 1;
+    return true;
+  }
+  if (z >= np) {  // every coded plane empty: the values are +0
+    pos += 9u + (uint32_t)np;
+    return true;
+  }
+  const int M0 = 31 - z, nbelow = np - z;  // planes M0 .. M0 - nbelow + 1
+  // group phase: one (n, 7 bits) lookup per plane while n < 3
+  uint64_t gw = w;
+  uint32_t off = 9u + (uint32_t)z, wbase = pos;
+  uint32_t n = 0, G = 0;
+  int j = 0;
+  while (n < 3 && j < nbelow && j < 8) {
+    if (off > 57u) {
+      wbase += off;
+      gw = lds_win64(sw, wbase);
+      off = 0;
+    }
+    const uint32_t e = dt7[(n << 7) | ((uint32_t)(gw >> off) & 127u)];
+    G |= (e & 15u) << (4 * j);
+    off += (e >> 4) & 15u;
+    n = e >> 8;
+    j++;
+  }
+  if (n < 3 && j < nbelow) return false;  // group phase longer than 8 planes
+  const uint32_t vpos = wbase + off;
+  const uint32_t t = (uint32_t)(nbelow - j);  // verbatim planes, 4 bits each
+  const uint32_t nb = 4u * t;                 // <= 128
+  uint64_t v0 = lds_win64(sw, vpos), v1 = 0;
+  if (nb > 64) v1 = lds_win64(sw, vpos + 64);
+  if (nb < 64) v0 &= (1ull << nb) - 1ull;
+  else if (nb < 128) v1 &= (1ull << (nb - 64)) - 1ull;
+  const uint32_t sft = 4u * (uint32_t)j;  // <= 32
+  const uint64_t Ylo = (uint64_t)G | (v0 << sft);
+  uint32_t u[4] = {0u, 0u, 0u, 0u};
+  window_to_coeffs(Ylo, M0, u);
+  if (nbelow > 16) {
+    const uint64_t Yhi = ((v0 >> 1) >> (63u - sft)) | (v1 << sft);
+    window_to_coeffs(Yhi, M0 - 16, u);
+  }
+  pos = vpos + nb;
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = (int32_t)((u[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+  inv_lift(q[0], q[1], q[2], q[3]);
+  const float sc = dequant_scale(emax);
+#pragma unroll
+  for (int i = 0; i < 4; i++) f[i] = sc * (float)q[i];
+  return true;
+}
+
+// One stage of the 8 x 8 transpose of float4 elements across the 8-lane groups of a wave (butterfly over lane bit D:
+// lanes exchange with lane ^ D the elements whose index differs from theirs in bit D). DPP moves, no LDS.
+template <int D>
+__device__ __forceinline__ void xpose8_stage(float (&g)[8][4], uint32_t lane)
+{
+  const bool hi = (lane & D) != 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (!(k & D)) continue;
+    const int a = k ^ D, b = k;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int send = __float_as_int(hi ? g[a][c] : g[b][c]);
+      int recv;
+      if constexpr (D == 1) {
+        recv = __builtin_amdgcn_mov_dpp(send, 0xB1, 0xf, 0xf, false);  // quad_perm [1, 0, 3, 2]
+      } else if constexpr (D == 2) {
+        recv = __builtin_amdgcn_mov_dpp(send, 0x4E, 0xf, 0xf, false);  // quad_perm [2, 3, 0, 1]
+      } else {
+        const int up = __builtin_amdgcn_mov_dpp(send, 0x104, 0xf, 0xf, false);  // row_shl:4 (lane + 4)
+        const int dn = __builtin_amdgcn_mov_dpp(send, 0x114, 0xf, 0xf, false);  // row_shr:4 (lane - 4)
+        recv = hi ? dn : up;
+      }
+      if (hi) g[a][c] = __int_as_float(recv);
+      else g[b][c] = __int_as_float(recv);
+    }
+  }
+}
+
+// One lane per 16-block index chunk, LANES chunks per workgroup, the workgroup's stream span staged in LDS (one round
+// trip, stage_lds16). A lane decodes its chunk in two rounds of eight blocks; an 8 x 8 transpose across each group of
+// 8 lanes (DPP) then gives lane 8q + m block m of the group's chunk 8q + i for i = 0..7, so every store instruction
+// writes whole 128-byte lines (8 lanes x 16 bytes of one chunk). Stored as decoded -- each lane's 16 bytes 256 bytes
+// apart, 64 lines per instruction -- the stores alone cost as much as the decode: 1 GiB in 0.37 ms against 0.19 ms
+// for full-line instructions (tools/ubench/store_pattern.hip, modes 1 / 4). Workgroups whose span exceeds the stage,
+// partial chunks and strided outputs take the general path.
+template <uint32_t LANES>
+__global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                             uint64_t in_words, const uint64_t* __restrict__ index,
+                                                             uint64_t nchunks, uint64_t base_bits,
+                                                             uint64_t* __restrict__ end_out)
+{
+  constexpr uint32_t CAP = LANES * 16 * 80 / 64;  // stream words the stage holds
+  __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
+  __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
+  const uint64_t w0 = ((base_bits + index[c0]) >> 6) & ~1ull;  // 16-byte aligned start
+  const uint64_t wend = c0 + LANES < nchunks ? ((base_bits + index[c0 + LANES] + 63) >> 6) : in_words;
+  const uint64_t span = min<uint64_t>(wend, in_words) - w0;
+  const bool staged = span <= CAP;
+  const uint64_t c = c0 + tid;
+  const uint64_t mine = c < nchunks ? index[c] : 0ull;
+  stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
+  if (staged) stage_lds16<LANES, (CAP + 4) / 2>(sw, in + w0, (uint32_t)(8 * span));
+  __syncthreads();
+  float* out = (float*)F.data;
+  const bool whole = c0 + LANES <= nchunks && 16 * (c0 + LANES) <= (uint64_t)F.n[0] / 4;  // no partial chunk or block
+  if (!staged || !whole || !F.vec) {  // the general path (wave-uniform: the whole workgroup)
+    if (c >= nchunks) return;
+    const uint64_t b0 = c * 16, b1 = min<uint64_t>(b0 + 16, F.nblocks);
+    uint64_t pos = base_bits + mine;
+    if (staged) {
+      pos -= 64 * w0;
+      for (uint64_t b = b0; b < b1; b++) {
+        float f[4];
+        decode_block1d_var(LdsWindow{sw}, pos, dt7, p.minexp, p.maxprec, f);
+        scatter_block<1>(F, (uint32_t)b, f);
+      }
+      pos += 64 * w0;
+    } else {
+      for (uint64_t b = b0; b < b1; b++) {
+        float f[4];
+        decode_block1d_var(GlobalWindow{in}, pos, dt7, p.minexp, p.maxprec, f);
+        scatter_block<1>(F, (uint32_t)b, f);
+      }
+    }
+    if (end_out && c == nchunks - 1) *end_out = pos;
+    return;
+  }
+  const uint32_t* sw32 = (const uint32_t*)sw;
+  const int cexp = 4 - p.minexp, maxprec = (int)min(p.maxprec, 64u);
+  uint32_t pos = (uint32_t)(base_bits + mine - 64 * w0);
+  const uint32_t lane = tid & 63u, m = lane & 7u;
+  float4* o4 = (float4*)out + (c - m) * 16 + m;  // block m of the group's first chunk
+#pragma unroll
+  for (int rnd = 0; rnd < 2; rnd++) {
+    float g[8][4];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (!dec_block1d_lean(sw32, pos, dt7, cexp, maxprec, g[k])) {
+        uint64_t p64 = pos;
+        decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, g[k]);
+        pos = (uint32_t)p64;
+      }
+    }
+    xpose8_stage<1>(g, lane);
+    xpose8_stage<2>(g, lane);
+    xpose8_stage<4>(g, lane);
+#pragma unroll
+    for (int i = 0; i < 8; i++) o4[16 * i + 8 * rnd] = make_float4(g[i][0], g[i][1], g[i][2], g[i][3]);
+  }
+  if (end_out && c == nchunks - 1) *end_out = pos + 64 * w0;
+}
+
 // the partial last block of a 1-D field (generic decoder, one lane)
 __global__ void k_decode_tail1d(FieldDesc F, Params p, const uint64_t* __restrict__ in, uint64_t base_bits,
                                 uint32_t b)
@@ -2257,8 +2446,8 @@ hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64
                                uint64_t* end_out, void* stream)
 {
   if (index && chunk == 16 && in_words) {  // the workgroup's stream span staged in LDS, 128 lanes
-    k_decode1d_var_staged<128><<<(uint32_t)((nchunks + 127) / 128), 128, 0, S(stream)>>>(F, p, in, in_words, index,
-                                                                                          nchunks, base_bits, end_out);
+    k_decode1d_var_lean<128><<<(uint32_t)((nchunks + 127) / 128), 128, 0, S(stream)>>>(F, p, in, in_words, index,
+                                                                                        nchunks, base_bits, end_out);
     return hipGetLastError();
   }
   k_decode1d_var<<<(uint32_t)((nchunks + 255) / 256), 256, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, base_bits,
