@@ -372,16 +372,37 @@ __device__ __forceinline__ pipe_v4u buf_load_b128(uint32_t off, pipe_v4i rs)
   return v;
 }
 
+// V (A/B builds): 1 = table loads first, 2 = lean6 variant coder, 4 = the whole LDS image as one constant
+#ifndef GCOW_C2_V
+#define GCOW_C2_V 3
+#endif
+
 template <int DT, uint32_t WB, int U, uint32_t T = 256, int V = 0>
 __global__ __launch_bounds__(T) void k_encode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
                                                          void* __restrict__ out)
 {
-  __shared__ uint32_t tab[1280 + 1024];  // pair table, then the four window spread tables
+  __shared__ __attribute__((aligned(16))) uint32_t tab[1280 + 1024];  // pair table, then the four window spread tables
   constexpr uint32_t IB = DT == DT_BF16 ? 8u : 16u;  // input bytes per block
   const pipe_v4i rin = buf_rsrc(in, nfull * IB), rout = buf_rsrc(out, nfull * (WB / 8));
   const uint32_t b0 = blockIdx.x * (T * U) + threadIdx.x;
   typename PipeRow<DT>::T r[U];
-  if constexpr ((V & 1) != 0) {
+  if constexpr ((V & 4) != 0) {
+    // the whole LDS image (pair table + spread tables, g_enc_tab1: 576 16-byte chunks, three per lane) requested
+    // first, hand-counted like the data loads: waiting for it is vmcnt(U), and no lane computes spread entries
+    static_assert(T == 256, "table fill assumes 256 threads");
+    constexpr uint32_t TCH = sizeof(EncTab1) / 16, TR = (TCH + 255) / 256;
+    static_assert(TR == 3, "the wait below ties three table registers");
+    const pipe_v4i rt = buf_rsrc(&g_enc_tab1, sizeof(EncTab1));
+    pipe_v4u tv[TR];
+#pragma unroll
+    for (uint32_t i = 0; i < TR; i++) tv[i] = buf_load_b128((threadIdx.x + 256u * i) * 16u, rt);
+#pragma unroll
+    for (int k = 0; k < U; k++) r[k] = PipeRow<DT>::load((b0 + T * k) * IB, rin);
+    asm volatile("s_waitcnt vmcnt(%3)" : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]) : "n"(U) : "memory");
+#pragma unroll
+    for (uint32_t i = 0; i < TR; i++)
+      if (threadIdx.x + 256u * i < TCH) ((pipe_v4u*)tab)[threadIdx.x + 256u * i] = tv[i];
+  } else if constexpr ((V & 1) != 0) {
     // pair-table loads issued first (hand-counted like the data loads), so waiting for them is vmcnt(U) and block 0
     // can start as soon as its own load lands (a compiler-issued table load after the data loads waits vmcnt(0))
     static_assert(T == 256, "table fill assumes 256 threads");
@@ -1643,7 +1664,10 @@ __device__ __forceinline__ uint64_t lds_win64(const uint32_t* w, uint32_t pos)
   return ((uint64_t)__builtin_amdgcn_alignbit(c, b, pos) << 32) | __builtin_amdgcn_alignbit(b, a, pos);
 }
 
-// returns false when the block needs the general decoder (pos unchanged then)
+// returns false when the block needs the general decoder (pos unchanged then). Written without data-dependent
+// branches where the work is small (zero and empty blocks run the coded path on masked values; the group phase is
+// a wave-uniform loop with a predicated body): a divergent if / loop costs the wave scalar exec-mask bookkeeping
+// (3-6 SALU each), and the staged decoders were issuing ~120 SALU per block that way.
 __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& pos, const uint16_t* dt7, int cexp,
                                                  int maxprec, float* f)
 {
@@ -1652,58 +1676,52 @@ __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& p
   const int np = min(32, min(maxprec, max(0, emax + cexp)));  // coded planes 31 .. 32 - np
   const uint64_t r = w >> 9;
   const int z = r ? (int)__builtin_ctzll(r) : 64;  // empty planes (any np <= 32 < 55 is covered)
-  f[0] = f[1] = f[2] = f[3] = 0.0f;
-  if (!(w & 1u)) {  // zero block (or no precision): one 0 bit
-    pos += 1;
-    return true;
-  }
-  if (z >= np) {  // every coded plane empty: the values are +0
-    pos += 9u + (uint32_t)np;
-    return true;
-  }
-  const int M0 = 31 - z, nbelow = np - z;  // planes M0 .. M0 - nbelow + 1
+  const bool nz = (w & 1u) != 0;                   // header bit: 0 = zero block, one bit
+  const bool coded = nz && z < np;                 // else every value is +0
+  const int M0 = 31 - z, nbelow = coded ? np - z : 0;  // planes M0 .. M0 - nbelow + 1
   // group phase: one (n, 7 bits) lookup per plane while n < 3
   uint64_t gw = w;
-  uint32_t off = 9u + (uint32_t)z, wbase = pos;
+  uint32_t off = 9u + (uint32_t)min(z, 48), wbase = pos;
   uint32_t n = 0, G = 0;
   int j = 0;
-  while (n < 3 && j < nbelow && j < 8) {
-    if (off > 57u) {
+#pragma unroll 1
+  for (int it = 0; it < 8; it++) {
+    const bool act = n < 3 && j < nbelow;
+    if (!__any(act)) break;
+    if (act && off > 57u) {  // rare: the next lookup's 7 bits run past the window
       wbase += off;
       gw = lds_win64(sw, wbase);
       off = 0;
     }
     const uint32_t e = dt7[(n << 7) | ((uint32_t)(gw >> off) & 127u)];
-    G |= (e & 15u) << (4 * j);
-    off += (e >> 4) & 15u;
-    n = e >> 8;
-    j++;
+    G = act ? G | ((e & 15u) << (4 * j)) : G;
+    off = act ? off + ((e >> 4) & 15u) : off;
+    n = act ? e >> 8 : n;
+    j = act ? j + 1 : j;
   }
-  if (n < 3 && j < nbelow) return false;  // group phase longer than 8 planes
+  const bool slow = n < 3 && j < nbelow;  // group phase longer than 8 planes
   const uint32_t vpos = wbase + off;
-  const uint32_t t = (uint32_t)(nbelow - j);  // verbatim planes, 4 bits each
-  const uint32_t nb = 4u * t;                 // <= 128
-  uint64_t v0 = lds_win64(sw, vpos), v1 = 0;
-  if (nb > 64) v1 = lds_win64(sw, vpos + 64);
-  if (nb < 64) v0 &= (1ull << nb) - 1ull;
-  else if (nb < 128) v1 &= (1ull << (nb - 64)) - 1ull;
+  const uint32_t nb = 4u * (uint32_t)(nbelow - j);  // verbatim planes, 4 bits each (<= 128)
+  uint64_t v0 = lds_win64(sw, vpos) & lowmask64(nb), v1 = 0;
+  if (nb > 64) v1 = lds_win64(sw, vpos + 64) & lowmask64(nb - 64);
   const uint32_t sft = 4u * (uint32_t)j;  // <= 32
   const uint64_t Ylo = (uint64_t)G | (v0 << sft);
   uint32_t u[4] = {0u, 0u, 0u, 0u};
-  window_to_coeffs(Ylo, M0, u);
+  window_to_coeffs(Ylo, M0 & 31, u);
   if (nbelow > 16) {
     const uint64_t Yhi = ((v0 >> 1) >> (63u - sft)) | (v1 << sft);
     window_to_coeffs(Yhi, M0 - 16, u);
   }
-  pos = vpos + nb;
   int32_t q[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) q[i] = (int32_t)((u[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
   inv_lift(q[0], q[1], q[2], q[3]);
-  const float sc = dequant_scale(emax);
+  // 2^(emax - 30) (0 below the subnormals, as dequant_scale), 0 for uncoded blocks
+  const float sc = coded ? __builtin_amdgcn_ldexpf(1.0f, emax - 30) : 0.0f;
 #pragma unroll
   for (int i = 0; i < 4; i++) f[i] = sc * (float)q[i];
-  return true;
+  pos = !nz ? pos + 1u : (!coded ? pos + 9u + (uint32_t)np : vpos + nb);
+  return !slow;
 }
 
 // One stage of the 8 x 8 transpose of float4 elements across the 8-lane groups of a wave (butterfly over lane bit D:
@@ -1796,8 +1814,9 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params
     float g[8][4];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
+      const uint32_t start = pos;
       if (!dec_block1d_lean(sw32, pos, dt7, cexp, maxprec, g[k])) {
-        uint64_t p64 = pos;
+        uint64_t p64 = start;
         decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, g[k]);
         pos = (uint32_t)p64;
       }
@@ -2030,7 +2049,7 @@ __global__ __launch_bounds__(256) void k_stitch_shards(uint64_t* __restrict__ ds
 // (any fixed rate). One block per lane.
 template <uint32_t WB>
 __global__ __launch_bounds__(256) void k_decode_mean_fixed1d(FieldDesc F, Params p, const uint64_t* __restrict__ in,
-                                                             uint64_t stream_words, uint32_t nstreams)
+                                                             uint64_t stream_words, uint32_t nstreams, uint64_t bfirst)
 {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) uint16_t dtab[WB ? 5 * 8 * 128 : 8];
@@ -2038,7 +2057,7 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d(FieldDesc F, Params
     stage_lds16<256, sizeof(DecTab1) / 16>(dtab, &g_dec_tab1, sizeof(DecTab1));
     __syncthreads();
   }
-  const uint64_t b = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const uint64_t b = bfirst + (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (b >= F.nblocks) return;
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   for (uint32_t r = 0; r < nstreams; r++) {
@@ -2060,13 +2079,194 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d(FieldDesc F, Params
   scatter_block<1>(F, (uint32_t)b, acc);
 }
 
+// The fixed-rate mean in the shape of k_decode_fixed1d_np (whole-word blocks, kmin = 0): one-shot, U blocks per lane
+// 256 apart, the plane table requested first; stream s + 1's U words are requested before stream s's blocks are
+// decoded, so each stream waits for its words with vmcnt(U) behind the next stream's loads (hand-counted, the loads
+// are raw buffer loads the compiler does not see). Full blocks only (the launcher sends a partial last block to
+// k_decode_mean_fixed1d).
+template <uint32_t WB, int U>
+__global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                                uint64_t stream_words, uint32_t nstreams,
+                                                                uint32_t nfull)
+{
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) uint16_t dtab[5 * 8 * 128];
+  constexpr uint32_t WBYTES = WB / 8;
+  const uint32_t b0 = blockIdx.x * (256u * U) + threadIdx.x;
+  constexpr uint32_t TCH = sizeof(DecTab1) / 16, TR = (TCH + 255) / 256;
+  const pipe_v4i rt = buf_rsrc(&g_dec_tab1, sizeof(DecTab1));
+  pipe_v4u tv[TR];
+#pragma unroll
+  for (uint32_t i = 0; i < TR; i++) tv[i] = buf_load_b128((threadIdx.x + 256u * i) * 16u, rt);
+  typename PipeWord<WB>::T rc[U], rn[U];
+  {
+    const pipe_v4i rs = buf_rsrc(in, nfull * WBYTES);
+#pragma unroll
+    for (int k = 0; k < U; k++) rc[k] = PipeWord<WB>::load((b0 + 256u * k) * WBYTES, rs);
+  }
+  static_assert(TR == 3, "the wait below ties three table registers");
+  asm volatile("s_waitcnt vmcnt(%3)" : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]) : "n"(U) : "memory");
+#pragma unroll
+  for (uint32_t i = 0; i < TR; i++)
+    if (threadIdx.x + 256u * i < TCH) ((pipe_v4u*)dtab)[threadIdx.x + 256u * i] = tv[i];
+  __syncthreads();
+  float acc[U][4];
+#pragma unroll
+  for (int k = 0; k < U; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
+  for (uint32_t r = 0; r < nstreams; r++) {
+    if (r + 1 < nstreams) {
+      const pipe_v4i rs = buf_rsrc(in + (uint64_t)(r + 1) * stream_words, nfull * WBYTES);
+#pragma unroll
+      for (int k = 0; k < U; k++) rn[k] = PipeWord<WB>::load((b0 + 256u * k) * WBYTES, rs);
+#pragma unroll
+      for (int k = 0; k < U; k++) pipe_wait<U>(rc[k]);  // the older U (this stream's) have landed
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; k++) pipe_wait<0>(rc[k]);
+    }
+    const uint64_t* sr = in + (uint64_t)r * stream_words;
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const uint32_t b = b0 + 256u * k;
+      float f[4];
+      bool special;
+      decode_block1d_fast<WB>(PipeWord<WB>::get(rc[k]), dtab, f, special);
+      if (special && b < nfull) {
+        BitReader rd{sr, (uint64_t)b * WB};
+        decode_block<1>(rd, p, f);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[k][i] = acc[k][i] + f[i];
+    }
+#pragma unroll
+    for (int k = 0; k < U; k++) rc[k] = rn[k];
+  }
+  const float nf = (float)nstreams;
+  float* out = (float*)F.data;
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    const uint32_t b = b0 + 256u * k;
+    if (b < nfull) {
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) v[i] = acc[k][i] / nf;
+      if (F.vec) *(float4*)(out + 4 * (uint64_t)b) = make_float4(v[0], v[1], v[2], v[3]);
+      else scatter_block<1>(F, b, v);
+    }
+  }
+}
+
+// Variable rate (1-D closed-form domain), the lean decoder's shape (k_decode1d_var_lean): LANES 16-block chunks per
+// workgroup; for each stream in rank order its span is staged in LDS (one round trip) and each lane decodes its chunk
+// into 64 registers of sums; the means leave through the 8 x 8 lane transposes as whole-line stores. Complete
+// workgroups only (whole chunks, full blocks, contiguous output); the launcher sends the rest to k_decode_mean1d_var.
+template <uint32_t LANES>
+__global__ __launch_bounds__(LANES) void k_decode_mean1d_var_lean(FieldDesc F, Params p,
+                                                                  const uint64_t* __restrict__ in,
+                                                                  uint64_t stream_words,
+                                                                  const uint64_t* __restrict__ index,
+                                                                  uint64_t index_words, uint64_t nchunks,
+                                                                  uint32_t nstreams)
+{
+#pragma clang fp contract(off)
+  constexpr uint32_t CAP = LANES * 16 * 80 / 64;
+  __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
+  __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
+  const uint64_t c = c0 + tid;
+  const uint32_t* sw32 = (const uint32_t*)sw;
+  const int cexp = 4 - p.minexp, maxprec = (int)min(p.maxprec, 64u);
+  stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
+  float a0[8][4], a1[8][4];
+#pragma unroll
+  for (int k = 0; k < 8; k++) a0[k][0] = a0[k][1] = a0[k][2] = a0[k][3] = a1[k][0] = a1[k][1] = a1[k][2] = a1[k][3] = 0.0f;
+  for (uint32_t r = 0; r < nstreams; r++) {
+    const uint64_t* sr = in + (uint64_t)r * stream_words;
+    const uint64_t* ix = index + (uint64_t)r * index_words;
+    // the staged span starts on a 16-byte boundary of the whole buffer (streams are stream_words apart, which may be
+    // odd): w0 may be one word before this stream's first word (the previous stream's last word, never decoded)
+    const uint64_t sbase = (uint64_t)r * stream_words;
+    const int64_t w0 = (int64_t)((sbase + (ix[c0] >> 6)) & ~1ull) - (int64_t)sbase;
+    const uint64_t wend = c0 + LANES < nchunks ? ((ix[c0 + LANES] + 63) >> 6) : stream_words;
+    const uint64_t mine = ix[c];
+    const uint64_t span = (uint64_t)((int64_t)min<uint64_t>(wend, stream_words) - w0);
+    const bool staged = span <= CAP;
+    __syncthreads();  // the previous stream's span is no longer read
+    if (staged) stage_lds16<LANES, (CAP + 4) / 2>(sw, sr + w0, (uint32_t)(8 * span));
+    __syncthreads();
+    if (staged) {
+      uint32_t pos = (uint32_t)((int64_t)mine - 64 * w0);
+#pragma unroll 1
+      for (int rnd = 0; rnd < 2; rnd++) {
+        float g[8][4];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const uint32_t start = pos;
+          if (!dec_block1d_lean(sw32, pos, dt7, cexp, maxprec, g[k])) {
+            uint64_t p64 = start;
+            decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, g[k]);
+            pos = (uint32_t)p64;
+          }
+        }
+        if (rnd == 0) {
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) a0[k][i] = a0[k][i] + g[k][i];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) a1[k][i] = a1[k][i] + g[k][i];
+        }
+      }
+    } else {  // a span past the stage (wave-uniform): from global memory, block by block
+      uint64_t pos = mine;
+#pragma unroll 1
+      for (int k = 0; k < 16; k++) {
+        float f[4];
+        decode_block1d_var(GlobalWindow{sr}, pos, dt7, p.minexp, p.maxprec, f);
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            a0[kk][i] = k == kk ? a0[kk][i] + f[i] : a0[kk][i];  // selects: + 0.0f would turn -0 into +0
+            a1[kk][i] = k == kk + 8 ? a1[kk][i] + f[i] : a1[kk][i];
+          }
+      }
+    }
+  }
+  const float nf = (float)nstreams;
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      a0[k][i] = a0[k][i] / nf;
+      a1[k][i] = a1[k][i] / nf;
+    }
+  const uint32_t lane = tid & 63u, m = lane & 7u;
+  float4* o4 = (float4*)F.data + (c - m) * 16 + m;
+  xpose8_stage<1>(a0, lane);
+  xpose8_stage<2>(a0, lane);
+  xpose8_stage<4>(a0, lane);
+#pragma unroll
+  for (int i = 0; i < 8; i++) o4[16 * i] = make_float4(a0[i][0], a0[i][1], a0[i][2], a0[i][3]);
+  xpose8_stage<1>(a1, lane);
+  xpose8_stage<2>(a1, lane);
+  xpose8_stage<4>(a1, lane);
+#pragma unroll
+  for (int i = 0; i < 8; i++) o4[16 * i + 8] = make_float4(a1[i][0], a1[i][1], a1[i][2], a1[i][3]);
+}
+
 // Variable rate (1-D closed-form domain) with each stream's block index every 16 blocks (index_words entries apart):
 // the shape of k_decode1d_var_staged -- LANES chunks of 16 blocks per workgroup, the workgroup's span of each stream
 // staged in LDS in turn -- with the 16 blocks' 64 values accumulated in registers across the streams and stored once.
 template <uint32_t LANES>
 __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params p, const uint64_t* __restrict__ in,
                                                              uint64_t stream_words, const uint64_t* __restrict__ index,
-                                                             uint64_t index_words, uint64_t nchunks, uint32_t nstreams)
+                                                             uint64_t index_words, uint64_t nchunks, uint32_t nstreams,
+                                                             uint64_t cfirst)
 {
 #pragma clang fp contract(off)
   constexpr uint32_t CAP = LANES * 16 * 80 / 64;
@@ -2074,7 +2274,7 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
   __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
   const uint32_t tid = threadIdx.x;
   stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
-  const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
+  const uint64_t c0 = cfirst + (uint64_t)blockIdx.x * LANES;
   const uint64_t c = c0 + tid;
   const uint64_t b0 = c * 16, b1 = min<uint64_t>(b0 + 16, F.nblocks);
   float acc[16][4];
@@ -2317,7 +2517,7 @@ static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, vo
         const uint32_t nc = min(CH, nfull - c0);
         const void* ic = (const char*)in + (size_t)c0 * IB;
         void* oc = (char*)out + (size_t)c0 * (WB / 8);
-        k_encode_fixed1d_np<DT, WB, 8, 256, 3><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
+        k_encode_fixed1d_np<DT, WB, 8, 256, GCOW_C2_V><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
       }
     }
   }
@@ -2527,11 +2727,25 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
   if (!F.nblocks) return hipSuccess;
   hipStream_t st = S(stream);
   if (p.minbits == p.maxbits) {
-    const uint32_t g = (F.nblocks + 255) / 256;
-    const bool lean = p.maxprec >= 32 && p.minexp <= -154;
-    if (lean && p.maxbits == 64) k_decode_mean_fixed1d<64><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams);
-    else if (lean && p.maxbits == 32) k_decode_mean_fixed1d<32><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams);
-    else k_decode_mean_fixed1d<0><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams);
+    const bool lean = p.maxprec >= 32 && p.minexp <= -154 && (p.maxbits == 64 || p.maxbits == 32);
+    const uint32_t nfull = (uint32_t)(F.n[0] / 4);
+    uint64_t done = 0;
+    if (lean && nfull && F.nblocks < (1u << 27)) {  // one-shot grid, U = 4 blocks per lane (buffer offsets < 2^32)
+      constexpr int U = 4;
+      const uint32_t g = (nfull + 256 * U - 1) / (256 * U);
+      if (p.maxbits == 64) k_decode_mean_fixed1d_np<64, U><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams, nfull);
+      else k_decode_mean_fixed1d_np<32, U><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams, nfull);
+      done = nfull;
+    }
+    const uint64_t rest = F.nblocks - done;
+    if (rest) {
+      const uint32_t g = (uint32_t)((rest + 255) / 256);
+      if (p.maxprec >= 32 && p.minexp <= -154 && p.maxbits == 64)
+        k_decode_mean_fixed1d<64><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams, done);
+      else if (p.maxprec >= 32 && p.minexp <= -154 && p.maxbits == 32)
+        k_decode_mean_fixed1d<32><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams, done);
+      else k_decode_mean_fixed1d<0><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams, done);
+    }
     return hipGetLastError();
   }
   const uint64_t nchunks = (F.nblocks + 15) / 16;
@@ -2540,8 +2754,20 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
                                                                               index_words, nchunks, nstreams);
     return hipGetLastError();
   }
-  k_decode_mean1d_var<128><<<(uint32_t)((nchunks + 127) / 128), 128, 0, st>>>(F, p, in, stream_words, index,
-                                                                               index_words, nchunks, nstreams);
+  // complete workgroups (128 whole chunks of full blocks, contiguous output) by the lean kernel, the rest by the
+  // general one
+  uint64_t nlean = 0;
+  if (F.vec) {
+    const uint64_t fullchunks = (F.n[0] / 4) / 16;
+    nlean = std::min<uint64_t>(fullchunks, nchunks) / 128;
+    if (nlean)
+      k_decode_mean1d_var_lean<128><<<(uint32_t)nlean, 128, 0, st>>>(F, p, in, stream_words, index, index_words,
+                                                                      nchunks, nstreams);
+  }
+  const uint64_t cfirst = nlean * 128;
+  if (cfirst < nchunks)
+    k_decode_mean1d_var<128><<<(uint32_t)((nchunks - cfirst + 127) / 128), 128, 0, st>>>(
+        F, p, in, stream_words, index, index_words, nchunks, nstreams, cfirst);
   return hipGetLastError();
 }
 
