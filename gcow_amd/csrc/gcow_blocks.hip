@@ -17,6 +17,7 @@ namespace gcow {
 // bit offset -- before the budget check stops the lane.
 constexpr uint32_t E3_SLACK = 8;
 
+
 // ------------------------------------------------------------------------------------------------ 3-D fixed rate
 // Fixed-rate 3-D blocks whose budget is a whole number of 32-bit words (maxbits = 32 WPB; rates 1, 2, 4, 8, 16, 32):
 // one block per lane, 256 consecutive blocks per workgroup. The lane codes its block (generic 64-coefficient coder,
@@ -34,12 +35,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   const uint32_t tid = threadIdx.x;
   const uint32_t b0 = blockIdx.x * 256u;
   const uint32_t nvalid = min(256u, F.nblocks - b0);
+  // the block's values requested with the E table, before the barrier
+  float f[64];
+  if (tid < nvalid) gather_block<3, DT>(F, b0 + tid, f);
   dup[tid] = g_dup_tab.v[tid];
   for (uint32_t j = tid; j < 64 * STRIDE; j += 256) ((uint4*)lds_w)[j] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   if (tid < nvalid) {
-    float f[64];
-    gather_block<3, DT>(F, b0 + tid, f);
     OrWriter w{lds_w + tid * STRIDE, 0u};
     encode_block<3>(w, f, p, dup);
   }

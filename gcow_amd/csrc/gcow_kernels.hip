@@ -372,11 +372,6 @@ __device__ __forceinline__ pipe_v4u buf_load_b128(uint32_t off, pipe_v4i rs)
   return v;
 }
 
-// V (A/B builds): 1 = table loads first, 2 = lean6 variant coder, 4 = the whole LDS image as one constant
-#ifndef GCOW_C2_V
-#define GCOW_C2_V 3
-#endif
-
 template <int DT, uint32_t WB, int U, uint32_t T = 256, int V = 0>
 __global__ __launch_bounds__(T) void k_encode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
                                                          void* __restrict__ out)
@@ -386,23 +381,7 @@ __global__ __launch_bounds__(T) void k_encode_fixed1d_np(const void* __restrict_
   const pipe_v4i rin = buf_rsrc(in, nfull * IB), rout = buf_rsrc(out, nfull * (WB / 8));
   const uint32_t b0 = blockIdx.x * (T * U) + threadIdx.x;
   typename PipeRow<DT>::T r[U];
-  if constexpr ((V & 4) != 0) {
-    // the whole LDS image (pair table + spread tables, g_enc_tab1: 576 16-byte chunks, three per lane) requested
-    // first, hand-counted like the data loads: waiting for it is vmcnt(U), and no lane computes spread entries
-    static_assert(T == 256, "table fill assumes 256 threads");
-    constexpr uint32_t TCH = sizeof(EncTab1) / 16, TR = (TCH + 255) / 256;
-    static_assert(TR == 3, "the wait below ties three table registers");
-    const pipe_v4i rt = buf_rsrc(&g_enc_tab1, sizeof(EncTab1));
-    pipe_v4u tv[TR];
-#pragma unroll
-    for (uint32_t i = 0; i < TR; i++) tv[i] = buf_load_b128((threadIdx.x + 256u * i) * 16u, rt);
-#pragma unroll
-    for (int k = 0; k < U; k++) r[k] = PipeRow<DT>::load((b0 + T * k) * IB, rin);
-    asm volatile("s_waitcnt vmcnt(%3)" : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]) : "n"(U) : "memory");
-#pragma unroll
-    for (uint32_t i = 0; i < TR; i++)
-      if (threadIdx.x + 256u * i < TCH) ((pipe_v4u*)tab)[threadIdx.x + 256u * i] = tv[i];
-  } else if constexpr ((V & 1) != 0) {
+  if constexpr ((V & 1) != 0) {
     // pair-table loads issued first (hand-counted like the data loads), so waiting for them is vmcnt(U) and block 0
     // can start as soon as its own load lands (a compiler-issued table load after the data loads waits vmcnt(0))
     static_assert(T == 256, "table fill assumes 256 threads");
@@ -1664,10 +1643,7 @@ __device__ __forceinline__ uint64_t lds_win64(const uint32_t* w, uint32_t pos)
   return ((uint64_t)__builtin_amdgcn_alignbit(c, b, pos) << 32) | __builtin_amdgcn_alignbit(b, a, pos);
 }
 
-// returns false when the block needs the general decoder (pos unchanged then). Written without data-dependent
-// branches where the work is small (zero and empty blocks run the coded path on masked values; the group phase is
-// a wave-uniform loop with a predicated body): a divergent if / loop costs the wave scalar exec-mask bookkeeping
-// (3-6 SALU each), and the staged decoders were issuing ~120 SALU per block that way.
+// returns false when the block needs the general decoder (pos unchanged then)
 __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& pos, const uint16_t* dt7, int cexp,
                                                  int maxprec, float* f)
 {
@@ -1676,52 +1652,58 @@ __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& p
   const int np = min(32, min(maxprec, max(0, emax + cexp)));  // coded planes 31 .. 32 - np
   const uint64_t r = w >> 9;
   const int z = r ? (int)__builtin_ctzll(r) : 64;  // empty planes (any np <= 32 < 55 is covered)
-  const bool nz = (w & 1u) != 0;                   // header bit: 0 = zero block, one bit
-  const bool coded = nz && z < np;                 // else every value is +0
-  const int M0 = 31 - z, nbelow = coded ? np - z : 0;  // planes M0 .. M0 - nbelow + 1
+  f[0] = f[1] = f[2] = f[3] = 0.0f;
+  if (!(w & 1u)) {  // zero block (or no precision): one 0 bit
+    pos += 1;
+    return true;
+  }
+  if (z >= np) {  // every coded plane empty: the values are +0
+    pos += 9u + (uint32_t)np;
+    return true;
+  }
+  const int M0 = 31 - z, nbelow = np - z;  // planes M0 .. M0 - nbelow + 1
   // group phase: one (n, 7 bits) lookup per plane while n < 3
   uint64_t gw = w;
-  uint32_t off = 9u + (uint32_t)min(z, 48), wbase = pos;
+  uint32_t off = 9u + (uint32_t)z, wbase = pos;
   uint32_t n = 0, G = 0;
   int j = 0;
-#pragma unroll 1
-  for (int it = 0; it < 8; it++) {
-    const bool act = n < 3 && j < nbelow;
-    if (!__any(act)) break;
-    if (act && off > 57u) {  // rare: the next lookup's 7 bits run past the window
+  while (n < 3 && j < nbelow && j < 8) {
+    if (off > 57u) {
       wbase += off;
       gw = lds_win64(sw, wbase);
       off = 0;
     }
     const uint32_t e = dt7[(n << 7) | ((uint32_t)(gw >> off) & 127u)];
-    G = act ? G | ((e & 15u) << (4 * j)) : G;
-    off = act ? off + ((e >> 4) & 15u) : off;
-    n = act ? e >> 8 : n;
-    j = act ? j + 1 : j;
+    G |= (e & 15u) << (4 * j);
+    off += (e >> 4) & 15u;
+    n = e >> 8;
+    j++;
   }
-  const bool slow = n < 3 && j < nbelow;  // group phase longer than 8 planes
+  if (n < 3 && j < nbelow) return false;  // group phase longer than 8 planes
   const uint32_t vpos = wbase + off;
-  const uint32_t nb = 4u * (uint32_t)(nbelow - j);  // verbatim planes, 4 bits each (<= 128)
-  uint64_t v0 = lds_win64(sw, vpos) & lowmask64(nb), v1 = 0;
-  if (nb > 64) v1 = lds_win64(sw, vpos + 64) & lowmask64(nb - 64);
+  const uint32_t t = (uint32_t)(nbelow - j);  // verbatim planes, 4 bits each
+  const uint32_t nb = 4u * t;                 // <= 128
+  uint64_t v0 = lds_win64(sw, vpos), v1 = 0;
+  if (nb > 64) v1 = lds_win64(sw, vpos + 64);
+  if (nb < 64) v0 &= (1ull << nb) - 1ull;
+  else if (nb < 128) v1 &= (1ull << (nb - 64)) - 1ull;
   const uint32_t sft = 4u * (uint32_t)j;  // <= 32
   const uint64_t Ylo = (uint64_t)G | (v0 << sft);
   uint32_t u[4] = {0u, 0u, 0u, 0u};
-  window_to_coeffs(Ylo, M0 & 31, u);
+  window_to_coeffs(Ylo, M0, u);
   if (nbelow > 16) {
     const uint64_t Yhi = ((v0 >> 1) >> (63u - sft)) | (v1 << sft);
     window_to_coeffs(Yhi, M0 - 16, u);
   }
+  pos = vpos + nb;
   int32_t q[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) q[i] = (int32_t)((u[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
   inv_lift(q[0], q[1], q[2], q[3]);
-  // 2^(emax - 30) (0 below the subnormals, as dequant_scale), 0 for uncoded blocks
-  const float sc = coded ? __builtin_amdgcn_ldexpf(1.0f, emax - 30) : 0.0f;
+  const float sc = dequant_scale(emax);
 #pragma unroll
   for (int i = 0; i < 4; i++) f[i] = sc * (float)q[i];
-  pos = !nz ? pos + 1u : (!coded ? pos + 9u + (uint32_t)np : vpos + nb);
-  return !slow;
+  return true;
 }
 
 // One stage of the 8 x 8 transpose of float4 elements across the 8-lane groups of a wave (butterfly over lane bit D:
@@ -2080,10 +2062,28 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d(FieldDesc F, Params
 }
 
 // The fixed-rate mean in the shape of k_decode_fixed1d_np (whole-word blocks, kmin = 0): one-shot, U blocks per lane
-// 256 apart, the plane table requested first; stream s + 1's U words are requested before stream s's blocks are
-// decoded, so each stream waits for its words with vmcnt(U) behind the next stream's loads (hand-counted, the loads
-// are raw buffer loads the compiler does not see). Full blocks only (the launcher sends a partial last block to
+// 256 apart, the plane table requested first (raw loads, hand-counted wait); stream s + 1's U words are requested
+// before stream s's blocks are decoded. The stream words are compiler-visible buffer loads: they are carried across
+// the stream loop, and a value loaded by inline asm must not be carried (the loop's register copies would read the
+// destination before the load has written it). Full blocks only (the launcher sends a partial last block to
 // k_decode_mean_fixed1d).
+template <uint32_t WB> struct MeanWord;
+template <> struct MeanWord<64> {
+  typedef uint64_t T;
+  static __device__ __forceinline__ T load(__amdgpu_buffer_rsrc_t rs, uint32_t b)
+  {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(b * 8u), 0, 0);
+    return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+  }
+};
+template <> struct MeanWord<32> {
+  typedef uint32_t T;
+  static __device__ __forceinline__ T load(__amdgpu_buffer_rsrc_t rs, uint32_t b)
+  {
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(b * 4u), 0, 0);
+  }
+};
+
 template <uint32_t WB, int U>
 __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Params p, const uint64_t* __restrict__ in,
                                                                 uint64_t stream_words, uint32_t nstreams,
@@ -2098,13 +2098,18 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
   pipe_v4u tv[TR];
 #pragma unroll
   for (uint32_t i = 0; i < TR; i++) tv[i] = buf_load_b128((threadIdx.x + 256u * i) * 16u, rt);
-  typename PipeWord<WB>::T rc[U], rn[U];
+  auto rsrc = [&](uint32_t r) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(in + (uint64_t)r * stream_words), 0, (int)(nfull * WBYTES),
+                                             0x00020000);
+  };
+  typename MeanWord<WB>::T cur[U];
   {
-    const pipe_v4i rs = buf_rsrc(in, nfull * WBYTES);
+    const auto rs = rsrc(0);
 #pragma unroll
-    for (int k = 0; k < U; k++) rc[k] = PipeWord<WB>::load((b0 + 256u * k) * WBYTES, rs);
+    for (int k = 0; k < U; k++) cur[k] = MeanWord<WB>::load(rs, b0 + 256u * k);
   }
   static_assert(TR == 3, "the wait below ties three table registers");
+  // the table loads are the oldest: once at most U loads are outstanding they have landed
   asm volatile("s_waitcnt vmcnt(%3)" : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]) : "n"(U) : "memory");
 #pragma unroll
   for (uint32_t i = 0; i < TR; i++)
@@ -2114,15 +2119,11 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
 #pragma unroll
   for (int k = 0; k < U; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
   for (uint32_t r = 0; r < nstreams; r++) {
+    typename MeanWord<WB>::T nxt[U];
     if (r + 1 < nstreams) {
-      const pipe_v4i rs = buf_rsrc(in + (uint64_t)(r + 1) * stream_words, nfull * WBYTES);
+      const auto rs = rsrc(r + 1);
 #pragma unroll
-      for (int k = 0; k < U; k++) rn[k] = PipeWord<WB>::load((b0 + 256u * k) * WBYTES, rs);
-#pragma unroll
-      for (int k = 0; k < U; k++) pipe_wait<U>(rc[k]);  // the older U (this stream's) have landed
-    } else {
-#pragma unroll
-      for (int k = 0; k < U; k++) pipe_wait<0>(rc[k]);
+      for (int k = 0; k < U; k++) nxt[k] = MeanWord<WB>::load(rs, b0 + 256u * k);
     }
     const uint64_t* sr = in + (uint64_t)r * stream_words;
 #pragma unroll
@@ -2130,7 +2131,7 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
       const uint32_t b = b0 + 256u * k;
       float f[4];
       bool special;
-      decode_block1d_fast<WB>(PipeWord<WB>::get(rc[k]), dtab, f, special);
+      decode_block1d_fast<WB>((uint64_t)cur[k], dtab, f, special);
       if (special && b < nfull) {
         BitReader rd{sr, (uint64_t)b * WB};
         decode_block<1>(rd, p, f);
@@ -2139,7 +2140,7 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
       for (int i = 0; i < 4; i++) acc[k][i] = acc[k][i] + f[i];
     }
 #pragma unroll
-    for (int k = 0; k < U; k++) rc[k] = rn[k];
+    for (int k = 0; k < U; k++) cur[k] = nxt[k];
   }
   const float nf = (float)nstreams;
   float* out = (float*)F.data;
@@ -2517,7 +2518,7 @@ static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, vo
         const uint32_t nc = min(CH, nfull - c0);
         const void* ic = (const char*)in + (size_t)c0 * IB;
         void* oc = (char*)out + (size_t)c0 * (WB / 8);
-        k_encode_fixed1d_np<DT, WB, 8, 256, GCOW_C2_V><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
+        k_encode_fixed1d_np<DT, WB, 8, 256, 3><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
       }
     }
   }
@@ -2730,7 +2731,10 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
     const bool lean = p.maxprec >= 32 && p.minexp <= -154 && (p.maxbits == 64 || p.maxbits == 32);
     const uint32_t nfull = (uint32_t)(F.n[0] / 4);
     uint64_t done = 0;
-    if (lean && nfull && F.nblocks < (1u << 27)) {  // one-shot grid, U = 4 blocks per lane (buffer offsets < 2^32)
+#ifndef GCOW_DMEAN_LEAN
+#define GCOW_DMEAN_LEAN 1
+#endif
+    if (GCOW_DMEAN_LEAN && lean && nfull && F.nblocks < (1u << 27)) {  // one-shot grid, U = 4 per lane
       constexpr int U = 4;
       const uint32_t g = (nfull + 256 * U - 1) / (256 * U);
       if (p.maxbits == 64) k_decode_mean_fixed1d_np<64, U><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams, nfull);

@@ -185,13 +185,6 @@ __host__ __device__ constexpr SpreadTab make_rspread()
 __device__ const SpreadTab g_rspread = make_rspread();
 
 // entry t of the spread tables computed in a kernel prologue (no table load): byte t & 255 onto nibble bit t >> 8
-__host__ __device__ constexpr uint32_t rspread_cx(uint32_t t)
-{
-  uint32_t v = 0;
-  for (uint32_t k = 0; k < 8; k++) v |= ((t >> k) & 1u) << (4 * (7 - k));
-  return v << (t >> 8);
-}
-
 __device__ __forceinline__ uint32_t rspread_entry(uint32_t t)
 {
   uint32_t v = 0;
@@ -200,23 +193,6 @@ __device__ __forceinline__ uint32_t rspread_entry(uint32_t t)
   return v << (t >> 8);
 }
 
-// The fixed-rate 1-D encoder's whole LDS image -- pair table (1280 entries) then the four spread tables (1024) -- as
-// one constant: a workgroup copies it with three 16-byte loads per lane instead of computing the 1024 spread entries
-// (~18 VALU each, 4 per lane per 2048-block workgroup: ~9 VALU per block).
-struct alignas(16) EncTab1 {
-  uint32_t v[1280 + 1024];
-};
-
-__host__ __device__ constexpr EncTab1 make_enc_tab1()
-{
-  EncTab1 T{};
-  const PlaneTab2 P = make_plane_tab5();
-  for (uint32_t t = 0; t < 1280; t++) T.v[t] = P.v[t];
-  for (uint32_t t = 0; t < 1024; t++) T.v[1280 + t] = rspread_cx(t);
-  return T;
-}
-
-__device__ const EncTab1 g_enc_tab1 = make_enc_tab1();
 
 // 16 planes from plane 31 of w (already shifted so the window's top plane is bit 31) down, as nibbles
 __device__ __forceinline__ uint64_t window_lds(const uint32_t* rs, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3)
