@@ -2084,7 +2084,7 @@ template <> struct MeanWord<32> {
   }
 };
 
-template <uint32_t WB, int U>
+template <uint32_t WB, int U, int D>
 __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Params p, const uint64_t* __restrict__ in,
                                                                 uint64_t stream_words, uint32_t nstreams,
                                                                 uint32_t nfull)
@@ -2102,15 +2102,20 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
     return __builtin_amdgcn_make_buffer_rsrc((void*)(in + (uint64_t)r * stream_words), 0, (int)(nfull * WBYTES),
                                              0x00020000);
   };
-  typename MeanWord<WB>::T cur[U];
+  typename MeanWord<WB>::T cur[U], nx1[U];
   {
     const auto rs = rsrc(0);
 #pragma unroll
     for (int k = 0; k < U; k++) cur[k] = MeanWord<WB>::load(rs, b0 + 256u * k);
+    if (D == 2 && nstreams > 1) {
+      const auto rs1 = rsrc(1);
+#pragma unroll
+      for (int k = 0; k < U; k++) nx1[k] = MeanWord<WB>::load(rs1, b0 + 256u * k);
+    }
   }
   static_assert(TR == 3, "the wait below ties three table registers");
-  // the table loads are the oldest: once at most U loads are outstanding they have landed
-  asm volatile("s_waitcnt vmcnt(%3)" : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]) : "n"(U) : "memory");
+  // the table loads are the oldest: once at most D U loads are outstanding they have landed
+  asm volatile("s_waitcnt vmcnt(%3)" : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]) : "n"(D * U) : "memory");
 #pragma unroll
   for (uint32_t i = 0; i < TR; i++)
     if (threadIdx.x + 256u * i < TCH) ((pipe_v4u*)dtab)[threadIdx.x + 256u * i] = tv[i];
@@ -2119,9 +2124,9 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
 #pragma unroll
   for (int k = 0; k < U; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
   for (uint32_t r = 0; r < nstreams; r++) {
-    typename MeanWord<WB>::T nxt[U];
-    if (r + 1 < nstreams) {
-      const auto rs = rsrc(r + 1);
+    typename MeanWord<WB>::T nxt[U];  // stream r + D's words
+    if (r + D < nstreams) {
+      const auto rs = rsrc(r + D);
 #pragma unroll
       for (int k = 0; k < U; k++) nxt[k] = MeanWord<WB>::load(rs, b0 + 256u * k);
     }
@@ -2140,7 +2145,14 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
       for (int i = 0; i < 4; i++) acc[k][i] = acc[k][i] + f[i];
     }
 #pragma unroll
-    for (int k = 0; k < U; k++) cur[k] = nxt[k];
+    for (int k = 0; k < U; k++) {
+      if (D == 2) {
+        cur[k] = nx1[k];
+        nx1[k] = nxt[k];
+      } else {
+        cur[k] = nxt[k];
+      }
+    }
   }
   const float nf = (float)nstreams;
   float* out = (float*)F.data;
@@ -2735,10 +2747,16 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
 #define GCOW_DMEAN_LEAN 1
 #endif
     if (GCOW_DMEAN_LEAN && lean && nfull && F.nblocks < (1u << 27)) {  // one-shot grid, U = 4 per lane
-      constexpr int U = 4;
+#ifndef GCOW_DMEAN_U
+#define GCOW_DMEAN_U 4
+#endif
+#ifndef GCOW_DMEAN_D
+#define GCOW_DMEAN_D 1
+#endif
+      constexpr int U = GCOW_DMEAN_U, D = GCOW_DMEAN_D;
       const uint32_t g = (nfull + 256 * U - 1) / (256 * U);
-      if (p.maxbits == 64) k_decode_mean_fixed1d_np<64, U><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams, nfull);
-      else k_decode_mean_fixed1d_np<32, U><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams, nfull);
+      if (p.maxbits == 64) k_decode_mean_fixed1d_np<64, U, D><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams, nfull);
+      else k_decode_mean_fixed1d_np<32, U, D><<<g, 256, 0, st>>>(F, p, in, stream_words, nstreams, nfull);
       done = nfull;
     }
     const uint64_t rest = F.nblocks - done;
