@@ -1740,15 +1740,22 @@ __device__ __forceinline__ void xpose8_stage(float (&g)[8][4], uint32_t lane)
 // 8 lanes (DPP) then gives lane 8q + m block m of the group's chunk 8q + i for i = 0..7, so every store instruction
 // writes whole 128-byte lines (8 lanes x 16 bytes of one chunk). Stored as decoded -- each lane's 16 bytes 256 bytes
 // apart, 64 lines per instruction -- the stores alone cost as much as the decode: 1 GiB in 0.37 ms against 0.19 ms
-// for full-line instructions (tools/ubench/store_pattern.hip, modes 1 / 4). Workgroups whose span exceeds the stage,
-// partial chunks and strided outputs take the general path.
+// for full-line instructions (tools/ubench/store_pattern.hip, modes 1 / 4).
+// The stage is sized for 64 bits per block on average (accuracy 1e-6 on gradient-scale data codes ~63), which sets the
+// occupancy (LDS-bound: 4.5 waves per SIMD at 64 bits, 3.5 at 80 -- C5 bucket 0.469 against 0.535 ms,
+// profiles/r04_var_decode_occupancy_ab.log). A workgroup whose span does not fit (a higher rate), partial chunks and
+// strided outputs take the general path (global-memory windows; staging such a workgroup in 2 or 4 parts instead
+// measured slower on the common path, profiles/r04_var_decode_parts_negative.log).
 template <uint32_t LANES>
 __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params p, const uint64_t* __restrict__ in,
                                                              uint64_t in_words, const uint64_t* __restrict__ index,
                                                              uint64_t nchunks, uint64_t base_bits,
                                                              uint64_t* __restrict__ end_out)
 {
-  constexpr uint32_t CAP = LANES * 16 * 80 / 64;  // stream words the stage holds
+#ifndef GCOW_VDEC_CAPB
+#define GCOW_VDEC_CAPB 64
+#endif
+  constexpr uint32_t CAP = LANES * 16 * GCOW_VDEC_CAPB / 64;  // stream words the stage holds (64 bits per block)
   __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
   __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
   const uint32_t tid = threadIdx.x;
@@ -2169,12 +2176,16 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
   }
 }
 
+#ifndef GCOW_DMV_WAVES
+#define GCOW_DMV_WAVES 4
+#endif
 // Variable rate (1-D closed-form domain), the lean decoder's shape (k_decode1d_var_lean): LANES 16-block chunks per
-// workgroup; for each stream in rank order its span is staged in LDS (one round trip) and each lane decodes its chunk
-// into 64 registers of sums; the means leave through the 8 x 8 lane transposes as whole-line stores. Complete
-// workgroups only (whole chunks, full blocks, contiguous output); the launcher sends the rest to k_decode_mean1d_var.
-template <uint32_t LANES>
-__global__ __launch_bounds__(LANES) void k_decode_mean1d_var_lean(FieldDesc F, Params p,
+// workgroup; for each stream in rank order its span is staged in LDS (in 1, 2 or 4 parts, as there) and each lane
+// decodes its chunk into 64 registers of sums; the means leave through the 8 x 8 lane transposes as whole-line
+// stores. Complete workgroups only (whole chunks, full blocks, contiguous output); the launcher sends the rest to
+// k_decode_mean1d_var.
+template <uint32_t LANES, uint32_t CAPB>
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_WAVES, 8))) void k_decode_mean1d_var_lean(FieldDesc F, Params p,
                                                                   const uint64_t* __restrict__ in,
                                                                   uint64_t stream_words,
                                                                   const uint64_t* __restrict__ index,
@@ -2182,7 +2193,8 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var_lean(FieldDesc F, P
                                                                   uint32_t nstreams)
 {
 #pragma clang fp contract(off)
-  constexpr uint32_t CAP = LANES * 16 * 80 / 64;
+  constexpr uint32_t CAP = LANES * 16 * CAPB / 64;
+  static_assert(LANES % 32 == 0 && CAP >= 32 * 16 * 140 / 64 + 4, "a quarter workgroup's longest span must fit");
   __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
   __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
   const uint32_t tid = threadIdx.x;
@@ -2191,85 +2203,62 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var_lean(FieldDesc F, P
   const uint32_t* sw32 = (const uint32_t*)sw;
   const int cexp = 4 - p.minexp, maxprec = (int)min(p.maxprec, 64u);
   stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
-  float a0[8][4], a1[8][4];
+  float acc[16][4];
 #pragma unroll
-  for (int k = 0; k < 8; k++) a0[k][0] = a0[k][1] = a0[k][2] = a0[k][3] = a1[k][0] = a1[k][1] = a1[k][2] = a1[k][3] = 0.0f;
+  for (int k = 0; k < 16; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
   for (uint32_t r = 0; r < nstreams; r++) {
     const uint64_t* sr = in + (uint64_t)r * stream_words;
     const uint64_t* ix = index + (uint64_t)r * index_words;
-    // the staged span starts on a 16-byte boundary of the whole buffer (streams are stream_words apart, which may be
-    // odd): w0 may be one word before this stream's first word (the previous stream's last word, never decoded)
     const uint64_t sbase = (uint64_t)r * stream_words;
-    const int64_t w0 = (int64_t)((sbase + (ix[c0] >> 6)) & ~1ull) - (int64_t)sbase;
-    const uint64_t wend = c0 + LANES < nchunks ? ((ix[c0 + LANES] + 63) >> 6) : stream_words;
+    // a span starts on a 16-byte boundary of the whole buffer (streams are stream_words apart, which may be odd):
+    // w0 may be one word before this stream's first word (the previous stream's last word, never decoded)
+    auto w_first = [&](uint64_t a) { return (int64_t)((sbase + (ix[a] >> 6)) & ~1ull) - (int64_t)sbase; };
+    auto w_end = [&](uint64_t b) { return (int64_t)min<uint64_t>(b < nchunks ? (ix[b] + 63) >> 6 : stream_words, stream_words); };
     const uint64_t mine = ix[c];
-    const uint64_t span = (uint64_t)((int64_t)min<uint64_t>(wend, stream_words) - w0);
-    const bool staged = span <= CAP;
-    __syncthreads();  // the previous stream's span is no longer read
-    if (staged) stage_lds16<LANES, (CAP + 4) / 2>(sw, sr + w0, (uint32_t)(8 * span));
-    __syncthreads();
-    if (staged) {
+    uint32_t P = 4;
+    if (w_end(c0 + LANES) - w_first(c0) <= (int64_t)CAP) P = 1;
+    else if (w_end(c0 + LANES / 2) - w_first(c0) <= (int64_t)CAP && w_end(c0 + LANES) - w_first(c0 + LANES / 2) <= (int64_t)CAP)
+      P = 2;
+    const uint32_t per = LANES / P;
+    for (uint32_t part = 0; part < P; part++) {
+      const uint64_t a = c0 + part * per;
+      const int64_t w0 = w_first(a);
+      const uint64_t span = (uint64_t)(w_end(a + per) - w0);
+      __syncthreads();  // the previous span is no longer read
+      stage_lds16<LANES, (CAP + 4) / 2>(sw, sr + w0, (uint32_t)(8 * span));
+      __syncthreads();
+      if (tid / per != part) continue;
       uint32_t pos = (uint32_t)((int64_t)mine - 64 * w0);
-#pragma unroll 1
-      for (int rnd = 0; rnd < 2; rnd++) {
-        float g[8][4];
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const uint32_t start = pos;
-          if (!dec_block1d_lean(sw32, pos, dt7, cexp, maxprec, g[k])) {
-            uint64_t p64 = start;
-            decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, g[k]);
-            pos = (uint32_t)p64;
-          }
-        }
-        if (rnd == 0) {
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) a0[k][i] = a0[k][i] + g[k][i];
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) a1[k][i] = a1[k][i] + g[k][i];
-        }
-      }
-    } else {  // a span past the stage (wave-uniform): from global memory, block by block
-      uint64_t pos = mine;
-#pragma unroll 1
       for (int k = 0; k < 16; k++) {
+        const uint32_t start = pos;
         float f[4];
-        decode_block1d_var(GlobalWindow{sr}, pos, dt7, p.minexp, p.maxprec, f);
+        if (!dec_block1d_lean(sw32, pos, dt7, cexp, maxprec, f)) {
+          uint64_t p64 = start;
+          decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, f);
+          pos = (uint32_t)p64;
+        }
 #pragma unroll
-        for (int kk = 0; kk < 8; kk++)
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            a0[kk][i] = k == kk ? a0[kk][i] + f[i] : a0[kk][i];  // selects: + 0.0f would turn -0 into +0
-            a1[kk][i] = k == kk + 8 ? a1[kk][i] + f[i] : a1[kk][i];
-          }
+        for (int i = 0; i < 4; i++) acc[k][i] = acc[k][i] + f[i];
       }
     }
   }
   const float nf = (float)nstreams;
-#pragma unroll
-  for (int k = 0; k < 8; k++)
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      a0[k][i] = a0[k][i] / nf;
-      a1[k][i] = a1[k][i] / nf;
-    }
   const uint32_t lane = tid & 63u, m = lane & 7u;
   float4* o4 = (float4*)F.data + (c - m) * 16 + m;
-  xpose8_stage<1>(a0, lane);
-  xpose8_stage<2>(a0, lane);
-  xpose8_stage<4>(a0, lane);
 #pragma unroll
-  for (int i = 0; i < 8; i++) o4[16 * i] = make_float4(a0[i][0], a0[i][1], a0[i][2], a0[i][3]);
-  xpose8_stage<1>(a1, lane);
-  xpose8_stage<2>(a1, lane);
-  xpose8_stage<4>(a1, lane);
+  for (int rnd = 0; rnd < 2; rnd++) {
+    float g[8][4];
 #pragma unroll
-  for (int i = 0; i < 8; i++) o4[16 * i + 8] = make_float4(a1[i][0], a1[i][1], a1[i][2], a1[i][3]);
+    for (int k = 0; k < 8; k++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) g[k][i] = acc[8 * rnd + k][i] / nf;
+    xpose8_stage<1>(g, lane);
+    xpose8_stage<2>(g, lane);
+    xpose8_stage<4>(g, lane);
+#pragma unroll
+    for (int i = 0; i < 8; i++) o4[16 * i + 8 * rnd] = make_float4(g[i][0], g[i][1], g[i][2], g[i][3]);
+  }
 }
 
 // Variable rate (1-D closed-form domain) with each stream's block index every 16 blocks (index_words entries apart):
@@ -2659,8 +2648,9 @@ hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64
                                uint64_t* end_out, void* stream)
 {
   if (index && chunk == 16 && in_words) {  // the workgroup's stream span staged in LDS, 128 lanes
-    k_decode1d_var_lean<128><<<(uint32_t)((nchunks + 127) / 128), 128, 0, S(stream)>>>(F, p, in, in_words, index,
-                                                                                        nchunks, base_bits, end_out);
+    constexpr uint32_t L = 128;
+    k_decode1d_var_lean<L><<<(uint32_t)((nchunks + L - 1) / L), L, 0, S(stream)>>>(F, p, in, in_words, index, nchunks,
+                                                                                  base_bits, end_out);
     return hipGetLastError();
   }
   k_decode1d_var<<<(uint32_t)((nchunks + 255) / 256), 256, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, base_bits,
@@ -2783,8 +2773,8 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
     const uint64_t fullchunks = (F.n[0] / 4) / 16;
     nlean = std::min<uint64_t>(fullchunks, nchunks) / 128;
     if (nlean)
-      k_decode_mean1d_var_lean<128><<<(uint32_t)nlean, 128, 0, st>>>(F, p, in, stream_words, index, index_words,
-                                                                      nchunks, nstreams);
+      k_decode_mean1d_var_lean<128, 64><<<(uint32_t)nlean, 128, 0, st>>>(F, p, in, stream_words, index, index_words,
+                                                                          nchunks, nstreams);
   }
   const uint64_t cfirst = nlean * 128;
   if (cfirst < nchunks)

@@ -721,6 +721,24 @@ def _var1d_form_case(gc, orc, mode):
     assert np.array_equal(d.cpu().numpy().view(np.uint32), orc.decompress(w_ref, a.shape, op).view(np.uint32))
 
 
+@pytest.mark.parametrize("bits", ["low", "mid", "high", "max"])
+def test_var1d_decode_stage_parts(gc, orc, bits):
+    """The lean 1-D variable-rate decoder stages a workgroup's stream (128 chunks of 16 blocks) in an LDS stage sized
+    for 64 bits per block; a workgroup above that takes the general path. Workgroups at ~24, ~63, ~110 and ~140 bits
+    per block, interleaved with low-rate ones, decode bit-exactly."""
+    rng = np.random.default_rng(4242)
+    wg = 128 * 16 * 4  # values per workgroup
+    n = wg * 6
+    a = rng.standard_normal(n).astype(np.float32)
+    scale = {"low": 1e-3, "mid": 1e-3, "high": 1.0, "max": 1.0}[bits]
+    a[wg:3 * wg] *= np.float32(scale)
+    a[:wg] *= np.float32(1e-6)
+    a[3 * wg:] *= np.float32(1e-5)
+    op = {"low": orc.accuracy(1e-3), "mid": orc.accuracy(1e-6), "high": orc.accuracy(1e-6),
+          "max": orc.precision(32)}[bits]
+    _check_vs_oracle(gc, orc, a, op, index_stride=16)
+
+
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("appended", [False, True])
 def test_var1d_mixed_tile_sizes(gc, orc, dtype, appended):
