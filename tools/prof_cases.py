@@ -2,7 +2,6 @@
 """Short, fixed-count runs of the C3 / C5 encoders for rocprofv3 kernel traces and PMC passes (few dispatches, so
 a counter pass stays within seconds).  usage: prof_cases.py [c2] [c3] [c5] [--reps N]"""
 import argparse
-import math
 import os
 import sys
 
@@ -27,14 +26,8 @@ def c2(reps):
 
 
 def c3(reps):
-    n = 512
-    g = torch.arange(n, device="cuda", dtype=torch.float64) / n
-    x = (torch.sin(6 * math.pi * g)[None, None, :] * torch.cos(4 * math.pi * g)[None, :, None] *
-         torch.sin(2 * math.pi * g)[:, None, None]).float()
-    noise = torch.empty(n ** 3, dtype=torch.float32, device="cuda")
-    codec.fill_normal(noise, 1e-3, inject=False)
-    x += noise.view(n, n, n)
-    del noise
+    """The C3 rate-8 and accuracy-1e-3 encode + decode pairs on the bench's C3 field (codec.c3_field)."""
+    x = codec.c3_field("cuda")
     for p, stride in ((codec.rate(8, 3), 0), (codec.accuracy(1e-3), 1)):
         enc = codec.Encoder(x.shape, torch.float32, p, index_stride=stride)
         out = torch.empty_like(x)
