@@ -386,11 +386,11 @@ def leg_host_e2e(ctx, enc, x, p, n, in_bytes, out_bytes):
         h_out[:nwo].copy_(e.words[:nwo], non_blocking=True)
 
     h_ms, _ = timed(ctx, seq, 2, 5)
-    henc = codec.HostEncoder(n, torch.float32, p, chunks=8, device=ctx.dev)
+    henc = codec.HostEncoder(n, torch.float32, p, chunks=16, device=ctx.dev)
     o_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 2, 5)
     return {"ms_per_step": round(h_ms, 3), "GiBps_input": round(gib(in_bytes, h_ms), 2),
             "overlapped_ms_per_step": round(o_ms, 3), "overlapped_GiBps_input": round(gib(in_bytes, o_ms), 2),
-            "note": "pinned hipMemcpyAsync H2D + encode + D2H, PCIe-inclusive (not `value`); overlapped = 8 chunks, "
+            "note": "pinned hipMemcpyAsync H2D + encode + D2H, PCIe-inclusive (not `value`); overlapped = 16 chunks, "
                     "H2D / encode / D2H on three streams (codec.HostEncoder)"}
 
 
@@ -459,7 +459,7 @@ def leg_configs(ctx):
         h_in = xb.cpu().pin_memory()
         h_out = torch.empty(codec.max_output_bytes((n,), p, torch.bfloat16) // 8 + 2, dtype=torch.int64,
                             pin_memory=True)
-        henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=8, device=ctx.dev)
+        henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=16, device=ctx.dev)
         h_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 2, 5)
         er = roof(n * 2, cbits / 8, k_ms,
                   "k_count1d_var_tile + k_scan_ranges_mw + k_encode1d_var_tile (+ k_encode1d_var_tile_big)")
@@ -479,7 +479,7 @@ def leg_configs(ctx):
                      "decode_ms": round(dk, 4), "decode_GiBps_output": round(gib(n * 4, dk), 2),
                      "decode_roofline": dr,
                      "host_path_ms": round(h_ms, 3), "host_path_GiBps_input": round(gib(n * 2, h_ms), 2),
-                     "host_path_note": "pinned bf16 H2D + encode + D2H of the stream, 8 overlapped chunks (PCIe-bound)"}
+                     "host_path_note": "pinned bf16 H2D + encode + D2H of the stream, 16 overlapped chunks (PCIe-bound: at 1e-6 the stream is as large as the bf16 input, so the D2H leg binds as much as the H2D; profiles/r04_host_chunks.log)"}
         del enc, h_in, h_out, henc, e, back
     del xb
     torch.cuda.empty_cache()

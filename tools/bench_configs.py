@@ -174,7 +174,7 @@ def c5():
         # overlapped host path: chunked H2D / encode / D2H on three streams (codec.HostEncoder)
         h_out2 = torch.empty(codec.max_output_bytes((n,), p, torch.bfloat16) // 8 + 2, dtype=torch.int64,
                              pin_memory=True)
-        henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=8)
+        henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=16)
         assert henc(h_in, h_out2) == bits
         ms_p = timeit(lambda: henc(h_in, h_out2), reps=3)
         emit(case="c5_bf16_acc%g" % tol, encode_ms=round(ms, 3),
