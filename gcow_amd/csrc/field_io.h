@@ -136,5 +136,40 @@ __device__ __forceinline__ void scatter_block(const FieldDesc& F, uint32_t b, co
   }
 }
 
+// fp32 -> bf16 bits, rounded to nearest even (torch's conversion; NaN -> 0x7fc0)
+__device__ __forceinline__ uint32_t bf16_rne(float x)
+{
+  const uint32_t u = __float_as_uint(x);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0u;
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// two values packed, lo in bits 0..15: gfx950's v_cvt_pk_bf16_f32 (round to nearest even, the default mode)
+__device__ __forceinline__ uint32_t bf16x2_rne(float lo, float hi)
+{
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+
+// One 1-D block of decoded values into the output field: fp32 (scatter_block), or bf16 (F.dtype == DT_BF16: each
+// value rounded to nearest even; one 8-byte store for a full block of a contiguous, 8-byte aligned field).
+__device__ __forceinline__ void store_block1d(const FieldDesc& F, uint64_t b, const float* v)
+{
+  if (F.dtype != DT_BF16) {
+    scatter_block<1>(F, (uint32_t)b, v);
+    return;
+  }
+  const uint64_t x0 = 4ull * b;
+  const uint32_t nv = (uint32_t)min<uint64_t>(4, F.n[0] - x0);
+  uint16_t* out = (uint16_t*)F.data;
+  if (nv == 4 && F.vec) {
+    *(uint2*)(out + x0) = make_uint2(bf16x2_rne(v[0], v[1]), bf16x2_rne(v[2], v[3]));
+  } else {
+#pragma unroll
+    for (uint32_t x = 0; x < 4u; x++)
+      if (x < nv) out[(int64_t)(x0 + x) * F.s[0]] = (uint16_t)bf16_rne(v[x]);
+  }
+}
 
 }  // namespace gcow

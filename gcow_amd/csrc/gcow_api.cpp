@@ -68,14 +68,16 @@ uint64_t block_bits_bound(const gcow_params& p, uint32_t dims)
   return std::max<uint64_t>(mb, std::max<uint64_t>(p.minbits, 1));
 }
 
-gcow_status make_field(const zfp_input* in, gcow::FieldDesc& F, bool for_decode)
+gcow_status make_field(const zfp_input* in, gcow::FieldDesc& F, bool for_decode, bool bf16_out = false)
 {
   if (!in) return fail(GCOW_ERR_INVALID, "null field");
   const uint32_t d = dims_of(in);
   if (d == 0) return fail(GCOW_ERR_INVALID, "field has no extents");
 
   if (for_decode) {
-    if (in->dtype != dtype_float) return fail(GCOW_ERR_UNSUPPORTED, "decode writes fp32 (dtype_float) only");
+    if (in->dtype != dtype_float && !(bf16_out && in->dtype == dtype_bf16))
+      return fail(GCOW_ERR_UNSUPPORTED, bf16_out ? "decode_mean writes dtype_float or dtype_bf16"
+                                                 : "decode writes fp32 (dtype_float) only");
   } else if (in->dtype != dtype_float && in->dtype != dtype_bf16) {
     return fail(GCOW_ERR_UNSUPPORTED, "encode supports dtype_float and dtype_bf16");
   }
@@ -976,7 +978,7 @@ gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p
                                     void* hip_stream)
 {
   gcow::FieldDesc F;
-  gcow_status st = make_field(field, F, true);
+  gcow_status st = make_field(field, F, true, true);
   if (st) return st;
   if ((st = check_params(p, 1))) return st;
   if (F.dims != 1) return fail(GCOW_ERR_UNSUPPORTED, "decode_mean is for 1-D buckets");

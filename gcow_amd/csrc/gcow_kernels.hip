@@ -2065,7 +2065,7 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d(FieldDesc F, Params
   const float nf = (float)nstreams;
 #pragma unroll
   for (int i = 0; i < 4; i++) acc[i] = acc[i] / nf;
-  scatter_block<1>(F, (uint32_t)b, acc);
+  store_block1d(F, b, acc);
 }
 
 // The fixed-rate mean in the shape of k_decode_fixed1d_np (whole-word blocks, kmin = 0): one-shot, U blocks per lane
@@ -2170,8 +2170,8 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) v[i] = acc[k][i] / nf;
-      if (F.vec) *(float4*)(out + 4 * (uint64_t)b) = make_float4(v[0], v[1], v[2], v[3]);
-      else scatter_block<1>(F, b, v);
+      if (F.vec && F.dtype != DT_BF16) *(float4*)(out + 4 * (uint64_t)b) = make_float4(v[0], v[1], v[2], v[3]);
+      else store_block1d(F, b, v);
     }
   }
 }
@@ -2246,6 +2246,8 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_
   const float nf = (float)nstreams;
   const uint32_t lane = tid & 63u, m = lane & 7u;
   float4* o4 = (float4*)F.data + (c - m) * 16 + m;
+  uint2* o2 = (uint2*)F.data + (c - m) * 16 + m;  // bf16 output: 8 bytes per block, a chunk is one 128-byte line
+  const bool bf = F.dtype == DT_BF16;
 #pragma unroll
   for (int rnd = 0; rnd < 2; rnd++) {
     float g[8][4];
@@ -2256,8 +2258,14 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_
     xpose8_stage<1>(g, lane);
     xpose8_stage<2>(g, lane);
     xpose8_stage<4>(g, lane);
+    if (bf) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) o4[16 * i + 8 * rnd] = make_float4(g[i][0], g[i][1], g[i][2], g[i][3]);
+      for (int i = 0; i < 8; i++)
+        o2[16 * i + 8 * rnd] = make_uint2(bf16x2_rne(g[i][0], g[i][1]), bf16x2_rne(g[i][2], g[i][3]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; i++) o4[16 * i + 8 * rnd] = make_float4(g[i][0], g[i][1], g[i][2], g[i][3]);
+    }
   }
 }
 
@@ -2325,8 +2333,8 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) v[i] = acc[k][i] / nf;
-      if (F.vec && 4 * b + 4 <= F.n[0]) *(float4*)(out + 4 * b) = make_float4(v[0], v[1], v[2], v[3]);
-      else scatter_block<1>(F, (uint32_t)b, v);
+      if (F.vec && F.dtype != DT_BF16 && 4 * b + 4 <= F.n[0]) *(float4*)(out + 4 * b) = make_float4(v[0], v[1], v[2], v[3]);
+      else store_block1d(F, b, v);
     }
   }
 }
@@ -2365,7 +2373,7 @@ __global__ __launch_bounds__(256) void k_decode_mean1d_generic(FieldDesc F, Para
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) v[i] = acc[k][i] / nf;
-      scatter_block<1>(F, (uint32_t)(b0 + k), v);
+      store_block1d(F, b0 + k, v);
     }
   }
 }

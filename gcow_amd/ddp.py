@@ -101,6 +101,15 @@ def _flat(buf: torch.Tensor):
     return flat, (flat if flat.dtype in (torch.float32, torch.bfloat16) else flat.float())
 
 
+def _mean_into(cdc, flat: torch.Tensor, *args):
+    """decode_mean written straight into the bucket when it is fp32 or bf16 (bf16: the fp32 mean rounded to nearest
+    even in the kernel -- no fp32 temporary, no cast pass); other dtypes through an fp32 temporary."""
+    if flat.dtype in (torch.float32, torch.bfloat16) and flat.is_contiguous():
+        cdc.decode_mean(*args, out=flat)
+    else:
+        flat.copy_(cdc.decode_mean(*args).to(flat.dtype))
+
+
 def roundtrip_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.Tensor]:
     """Mean all-reduce, then the lossy encode -> decode the reference applies (zfpy), device-resident."""
     group = state.process_group
@@ -195,8 +204,7 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
                 # the callback runs on a pool stream; without this the allocator could hand `gathered` to the next
                 # bucket's torch.zeros on the autograd stream before the decode below has read it
                 gathered.record_stream(torch.cuda.current_stream(gathered.device))
-            mean = cdc.decode_mean(gathered, nw, world, n, p)
-            flat.copy_(mean.to(flat.dtype))
+            _mean_into(cdc, flat, gathered, nw, world, n, p)
             return buf
 
         return fut.then(finish)
@@ -228,8 +236,7 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
             ni = index.numel()
             idx = torch.empty(world * ni, dtype=torch.int64, device=dev)
             gdist.allgather_into(idx, index[:ni].contiguous(), cgroup)
-            mean = cdc.decode_mean(gathered, maxw, world, n, p, idx, ni, INDEX_STRIDE)
-            flat.copy_(mean.to(flat.dtype))
+            _mean_into(cdc, flat, gathered, maxw, world, n, p, idx, ni, INDEX_STRIDE)
             # completed inside the side-stream context: the future records its event on this stream, so DDP's wait
             # orders its use of the bucket after the mean is written
             fut.set_result(buf)

@@ -264,8 +264,9 @@ gcow_status gcow_stitch_shards_device(uint64_t* d_dst, uint64_t dst_words, const
 
 /*
  * Decode-and-average of nstreams 1-D streams of one bucket shape (the compressed all-gather DDP hook's receive side;
- * hw/models/train_imagenet.py:446-475 is the caller contract): field->data (DEVICE fp32, 1-D) receives, elementwise
- * in fp32, ((0 + x_0) + x_1 + ... + x_{n-1}) / nstreams with x_r the libzfp decode of stream r. Streams start
+ * hw/models/train_imagenet.py:446-475 is the caller contract): field->data (DEVICE, 1-D, fp32 or bf16) receives,
+ * elementwise in fp32, ((0 + x_0) + x_1 + ... + x_{n-1}) / nstreams with x_r the libzfp decode of stream r (a bf16
+ * field -- a bf16 gradient bucket -- receives that fp32 mean rounded to nearest even, torch's conversion). Streams start
  * stream_words words apart at d_streams; streams_bytes is the buffer's size, which must cover nstreams * stream_words
  * + 2 words (the decoders read 64-bit windows past a stream's last bit; GCOW_ERR_INVALID otherwise). Fixed rate: any
  * parameters, d_index NULL and index_words = index_stride = 0. Variable rate: any parameters (minbits <= 1,

@@ -122,6 +122,43 @@ def test_decode_mean_vs_oracle(gc, orc, mode, world):
     assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
 
 
+def _bf16_rne(a: np.ndarray) -> np.ndarray:
+    """fp32 -> bf16 bits, round to nearest even (torch's conversion; the means here are finite)."""
+    u = a.view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+@pytest.mark.parametrize("mode", list(MEAN_MODES))
+@pytest.mark.parametrize("world", [1, 3])
+@pytest.mark.parametrize("layout", ["contiguous", "strided"])
+def test_decode_mean_bf16_output(gc, orc, mode, world, layout):
+    """decode_mean into a bf16 bucket (the hook's receive side for bf16 gradients): the fp32 mean of the oracle
+    decodes, rounded to nearest even, written in place -- contiguous (8-byte block stores, the lean kernels' transposed
+    stores) and strided (value stores)."""
+    n = 4 * 20001 + 2
+    op = _mean_op(orc, mode)
+    fixed = op.minbits == op.maxbits
+    buckets = [_bucket(orc, n, 700 + r, mode.startswith("bf16")) for r in range(world)]
+    encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else 16) for b in buckets]
+    sw = max((e.bits + 63) // 64 for e in encs) + (0 if fixed else 1)
+    streams = torch.zeros(world * sw + 2, dtype=torch.int64, device="cuda")
+    for r, e in enumerate(encs):
+        streams[r * sw:r * sw + e.nwords] = e.stream()
+    idx, ni = None, 0
+    if not fixed:
+        ni = encs[0].index.numel()
+        idx = torch.cat([e.index[:ni] for e in encs])
+    base = torch.full((2 * n,), -1.0, dtype=torch.bfloat16, device="cuda")
+    out = base[:n] if layout == "contiguous" else base[::2]
+    got = gc.decode_mean(streams, sw, world, n, _P(gc, op), idx, ni, 0 if fixed else 16, out=out)
+    want = _bf16_rne(_oracle_mean(orc, [orc.compress(b, op)[0] for b in buckets], op, n))
+    torch.cuda.synchronize()
+    assert got.data_ptr() == out.data_ptr()
+    assert np.array_equal(got.cpu().view(torch.int16).numpy().view(np.uint16), want)
+    untouched = base[n:] if layout == "contiguous" else base[1::2]
+    assert bool((untouched == -1.0).all())
+
+
 @pytest.mark.parametrize("mode", ["rate16", "acc1e-6"])
 def test_decode_mean_full_size_w8(gc, orc, mode):
     """The hook's receive side at the bench's size: 8 streams of 256 Mi fp32 values (8 different buckets, the bench's
@@ -338,6 +375,35 @@ def test_ddp_hooks_world1_bit_exact(gc, orc, nccl_world1, hook, mode):
             got = lm.weight.grad.reshape(-1).cpu().numpy()
             assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), step
     assert len(set(seen)) >= 2, seen  # several buckets per step
+
+
+@pytest.mark.parametrize("mode", ["rate16", "acc1e-6"])
+def test_ddp_allgather_hook_bf16_world1(gc, orc, nccl_world1, mode):
+    """bf16 model over RCCL: the all-gather hook decodes and averages straight into the bf16 bucket; every weight
+    gradient equals the oracle's decode of its (exactly widened) bf16 gradient, divided by 1 and rounded to nearest
+    even, bit for bit, over two steps and several buckets."""
+    from gcow_amd import ddp
+    params = gc.rate(16, 1) if mode == "rate16" else gc.accuracy(1e-6)
+    torch.manual_seed(0)
+    layers = lambda: torch.nn.Sequential(  # noqa: E731
+        *[torch.nn.Linear(768, 768, bias=False) for _ in range(3)]).cuda().to(torch.bfloat16)
+    model, ref = layers(), layers()
+    ref.load_state_dict(model.state_dict())
+    dm = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=1)
+    dm.register_comm_hook(ddp.GcowHookState(params=params), ddp.compressed_allgather_hook)
+    op = orc.expert(*params.tuple())
+    for step in range(2):
+        model.zero_grad()
+        ref.zero_grad()
+        x = torch.randn(32, 768, device="cuda", dtype=torch.bfloat16)
+        dm(x).float().square().mean().backward()
+        ref(x).float().square().mean().backward()
+        for lm, lr in zip(model, ref):
+            gb = lr.weight.grad.reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
+            dec = orc.decompress(orc.compress(gb, op)[0], gb.shape, op)
+            want = _bf16_rne((np.zeros_like(dec) + dec) / np.float32(1))
+            got = lm.weight.grad.reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
+            assert np.array_equal(got, want), step
 
 
 def test_allgather_hook_delayed_decode_stream(gc, orc, nccl_world1):

@@ -145,7 +145,13 @@ def decode_mean(W=8):
              GBps_write=round(n * 4 / (ms / 1e3) / 1e9, 1),
              GBps_read_write=round((n * 4 + cbytes) / (ms / 1e3) / 1e9, 1),
              bits_per_value=round(sum(lens) / W / n, 3))
-        del buf, streams, idx, enc
+        # a bf16 bucket: written in the kernel (rounded to nearest even) vs an fp32 temporary + cast + copy
+        ob = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+        ms_b = timeit(lambda: codec.decode_mean(buf, sw, W, n, p, ix, ni, stride, out=ob), reps=3)
+        ms_c = timeit(lambda: ob.copy_(codec.decode_mean(buf, sw, W, n, p, ix, ni, stride, out=out).to(torch.bfloat16)),
+                      reps=3)
+        emit(case="decode_mean_%s_W%d_bf16_out" % (name, W), ms=round(ms_b, 3), ms_fp32_then_cast=round(ms_c, 3))
+        del buf, streams, idx, enc, ob
 
 
 def c5():
