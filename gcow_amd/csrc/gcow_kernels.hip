@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1362,6 +1363,93 @@ __device__ __forceinline__ void decode_block1d_fast(uint64_t w, const uint16_t* 
   for (int i = 0; i < 4; i++) f[i] = nonzero ? sc * (float)q[i] : 0.0f;  // header bit 0: +0 whatever follows
 }
 
+#ifndef GCOW_DEC_PAIR
+#define GCOW_DEC_PAIR 1
+#endif
+// ---- two planes per lookup (64-bit blocks). The group phase lasts 1.5 planes on average on gradient-like data but
+// the wave-uniform loop above runs the wave's maximum (4.6 planes: profiles/r04_dec_pair_table.log), so each step
+// here decodes as many of the next two planes as the next 10 stream bits determine, and lanes step on their own.
+// Entry (n < 3, 10 bits): nibbles of plane 1 [0, 4) and plane 2 [4, 8), plane 1's length [8, 12), both planes'
+// length [12, 16), min(n, 3) after plane 1 [16, 18) and after plane 2 [18, 20), plane 2 decoded [20] (only when its
+// code ends inside the 10 bits: decoded with the bits past them zero, a code that stops before them read none).
+struct alignas(16) DecTabP {
+  uint32_t v[3 * 1024];
+};
+
+__host__ __device__ constexpr uint32_t dec_pair_cx(uint32_t t)
+{
+  const uint32_t n = t >> 10, b = t & 1023u;
+  const uint32_t e1 = dec_plane_cx((((n << 3) | 7u) << 7) | (b & 127u));
+  const uint32_t x1 = e1 & 15u, l1 = (e1 >> 4) & 15u, n1 = e1 >> 8;
+  const uint32_t e2 = dec_plane_cx((((n1 << 3) | 7u) << 7) | ((b >> l1) & 127u));
+  const uint32_t x2 = e2 & 15u, l2 = (e2 >> 4) & 15u, n2 = e2 >> 8;
+  const uint32_t r1 = n1 < 3 ? n1 : 3u, r2 = n2 < 3 ? n2 : 3u;
+  if (l1 + l2 <= 10u) return x1 | (x2 << 4) | (l1 << 8) | ((l1 + l2) << 12) | (r1 << 16) | (r2 << 18) | (1u << 20);
+  return x1 | (l1 << 8) | (l1 << 12) | (r1 << 16) | (r1 << 18);
+}
+
+__host__ __device__ constexpr DecTabP make_dec_pair()
+{
+  DecTabP T{};
+  for (uint32_t t = 0; t < 3 * 1024; t++) T.v[t] = dec_pair_cx(t);
+  return T;
+}
+
+__device__ const DecTabP g_dec_pair = make_dec_pair();
+
+// decode_block1d_fast<64> with the pair table: a lane leaves the loop when its group phase ends (n >= 3), its planes
+// run out (j > M0) or the 16-plane window is full; a plane that would cross the 64-bit budget goes to the generic
+// decoder (special), as does a group phase longer than the window.
+__device__ __forceinline__ void decode_block1d_pair(uint64_t w, const uint32_t* dtp, float* f, bool& special)
+{
+  const bool nonzero = w & 1u;
+  const int emax = (int)((w >> 1) & 255u) - 127;
+  const uint64_t r = w >> 9;
+  const int z = r ? (int)__builtin_ctzll(r) : 64;
+  const int M0 = 31 - z;  // < 0: every coded plane empty
+  uint32_t pos = 9u + (uint32_t)z;
+  uint64_t Y = 0;
+  uint32_t n = 0;
+  int j = 0;
+  bool cross = false;
+#pragma unroll
+  for (int it = 0; it < 16; it++) {
+    const uint32_t rem = 64u - min(pos, 64u);
+    const bool act = n < 3 && rem && j <= M0 && j < 16 && !cross;
+    if (!__any(act)) break;
+    if (act) {
+      const uint32_t e = dtp[(n << 10) | ((uint32_t)(w >> pos) & 1023u)];
+      const uint32_t l1 = (e >> 8) & 15u, l2 = (e >> 12) & 15u;
+      cross = l1 > rem;
+      const bool two = ((e >> 20) & 1u) && l2 <= rem && j < M0 && j < 15;
+      if (!cross) {
+        Y |= (uint64_t)(two ? (e & 255u) : (e & 15u)) << (4 * j);
+        pos += two ? l2 : l1;
+        n = (e >> (two ? 18 : 16)) & 3u;
+        j += two ? 2 : 1;
+      }
+    }
+  }
+  special = cross || (n < 3 && pos < 64u && j <= M0);  // budget inside a group plane, or a group phase past 16 planes
+  if (j < 16 && pos < 64u) Y |= (w >> pos) << (4 * j);  // verbatim nibbles (bits past the word are zero)
+  uint32_t u[4] = {0, 0, 0, 0};
+  if (M0 >= 0) {
+    window_to_coeffs(Y, M0, u);
+    const uint32_t p2 = pos + 4u * (uint32_t)(16 - min(j, 16));  // stream position of plane M0 - 16
+    if (__any(p2 < 64u && M0 >= 16)) {
+      const uint64_t Y2 = p2 < 64u && M0 >= 16 ? w >> p2 : 0ull;
+      if (M0 >= 16) window_to_coeffs(Y2, M0 - 16, u);
+    }
+  }
+  int32_t q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = (int32_t)((u[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+  inv_lift(q[0], q[1], q[2], q[3]);
+  const float sc = dequant_scale(emax);
+#pragma unroll
+  for (int i = 0; i < 4; i++) f[i] = nonzero ? sc * (float)q[i] : 0.0f;  // header bit 0: +0 whatever follows
+}
+
 template <uint32_t WB> struct PipeWord;
 template <> struct PipeWord<64> {
   typedef pipe_v2u T;
@@ -1391,7 +1479,12 @@ template <uint32_t WB, int U>
 __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
                                                            float* __restrict__ out, uint64_t base_bits)
 {
-  __shared__ __attribute__((aligned(16))) uint16_t dtab[5 * 8 * 128];
+  // (the pair table's unrolled group loop keeps this kernel's 16-block loop from being unrolled, and its counted waits
+  // need that; rolled, the pair loop was slower than the one-plane table: profiles/r04_dec_pair_table.log)
+  constexpr bool PAIR = false;
+  using Tab = DecTab1;
+  __shared__ __attribute__((aligned(16))) uint32_t dtab32[sizeof(Tab) / 4];
+  const uint16_t* dtab = (const uint16_t*)dtab32;
   constexpr uint32_t WBYTES = WB / 8;
   const pipe_v4i rin = buf_rsrc((const char*)in + base_bits / 8, nfull * WBYTES);
   const __amdgpu_buffer_rsrc_t rout_b = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(nfull * 16u), 0x00020000);
@@ -1399,8 +1492,8 @@ __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restric
   // the 10 KiB plane table (640 16-byte chunks, 3 per lane; the range check zeroes the rest) is requested first and
   // waited for with vmcnt(U): the U word loads behind it stay in flight, and no wait counts a memory round trip per
   // table chunk (as a compiler-issued copy loop does)
-  constexpr uint32_t TCH = sizeof(DecTab1) / 16, TR = (TCH + 255) / 256;
-  const pipe_v4i rt = buf_rsrc(&g_dec_tab1, sizeof(DecTab1));
+  constexpr uint32_t TCH = sizeof(Tab) / 16, TR = (TCH + 255) / 256;
+  const pipe_v4i rt = PAIR ? buf_rsrc(&g_dec_pair, sizeof(DecTabP)) : buf_rsrc(&g_dec_tab1, sizeof(DecTab1));
   pipe_v4u tv[TR];
 #pragma unroll
   for (uint32_t i = 0; i < TR; i++) tv[i] = buf_load_b128((threadIdx.x + 256u * i) * 16u, rt);
@@ -1411,7 +1504,7 @@ __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restric
   asm volatile("s_waitcnt vmcnt(%3)" : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]) : "n"(U) : "memory");
 #pragma unroll
   for (uint32_t i = 0; i < TR; i++)
-    if (threadIdx.x + 256u * i < TCH) ((pipe_v4u*)dtab)[threadIdx.x + 256u * i] = tv[i];
+    if (threadIdx.x + 256u * i < TCH) ((pipe_v4u*)dtab32)[threadIdx.x + 256u * i] = tv[i];
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < U; k++) {
@@ -1419,7 +1512,8 @@ __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restric
     const uint32_t b = b0 + 256u * k;
     float f[4];
     bool special;
-    decode_block1d_fast<WB>(PipeWord<WB>::get(r[k]), dtab, f, special);
+    if constexpr (PAIR) decode_block1d_pair(PipeWord<WB>::get(r[k]), dtab32, f, special);
+    else decode_block1d_fast<WB>(PipeWord<WB>::get(r[k]), dtab, f, special);
     if (special && b < nfull) {
       BitReader rd{(const uint64_t*)in, base_bits + (uint64_t)b * WB};
       decode_block<1>(rd, p, f);
@@ -1798,7 +1892,7 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params
   uint32_t pos = (uint32_t)(base_bits + mine - 64 * w0);
   const uint32_t lane = tid & 63u, m = lane & 7u;
   float4* o4 = (float4*)out + (c - m) * 16 + m;  // block m of the group's first chunk
-#pragma unroll
+#pragma unroll 1  // two copies of the 8-block body are past the unroller's size limit (nothing here needs them)
   for (int rnd = 0; rnd < 2; rnd++) {
     float g[8][4];
 #pragma unroll
@@ -2097,11 +2191,14 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
                                                                 uint32_t nfull)
 {
 #pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) uint16_t dtab[5 * 8 * 128];
+  constexpr bool PAIR = WB == 64 && GCOW_DEC_PAIR;  // 64-bit blocks: the two-plane table
+  using Tab = typename std::conditional<PAIR, DecTabP, DecTab1>::type;
+  __shared__ __attribute__((aligned(16))) uint32_t dtab32[sizeof(Tab) / 4];
+  const uint16_t* dtab = (const uint16_t*)dtab32;
   constexpr uint32_t WBYTES = WB / 8;
   const uint32_t b0 = blockIdx.x * (256u * U) + threadIdx.x;
-  constexpr uint32_t TCH = sizeof(DecTab1) / 16, TR = (TCH + 255) / 256;
-  const pipe_v4i rt = buf_rsrc(&g_dec_tab1, sizeof(DecTab1));
+  constexpr uint32_t TCH = sizeof(Tab) / 16, TR = (TCH + 255) / 256;
+  const pipe_v4i rt = PAIR ? buf_rsrc(&g_dec_pair, sizeof(DecTabP)) : buf_rsrc(&g_dec_tab1, sizeof(DecTab1));
   pipe_v4u tv[TR];
 #pragma unroll
   for (uint32_t i = 0; i < TR; i++) tv[i] = buf_load_b128((threadIdx.x + 256u * i) * 16u, rt);
@@ -2125,7 +2222,7 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
   asm volatile("s_waitcnt vmcnt(%3)" : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]) : "n"(D * U) : "memory");
 #pragma unroll
   for (uint32_t i = 0; i < TR; i++)
-    if (threadIdx.x + 256u * i < TCH) ((pipe_v4u*)dtab)[threadIdx.x + 256u * i] = tv[i];
+    if (threadIdx.x + 256u * i < TCH) ((pipe_v4u*)dtab32)[threadIdx.x + 256u * i] = tv[i];
   __syncthreads();
   float acc[U][4];
 #pragma unroll
@@ -2143,7 +2240,8 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
       const uint32_t b = b0 + 256u * k;
       float f[4];
       bool special;
-      decode_block1d_fast<WB>((uint64_t)cur[k], dtab, f, special);
+      if constexpr (PAIR) decode_block1d_pair((uint64_t)cur[k], dtab32, f, special);
+      else decode_block1d_fast<WB>((uint64_t)cur[k], dtab, f, special);
       if (special && b < nfull) {
         BitReader rd{sr, (uint64_t)b * WB};
         decode_block<1>(rd, p, f);

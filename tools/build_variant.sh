@@ -10,7 +10,7 @@ CS=$ROOT/gcow_amd/csrc
 OBJ=/tmp/gcow_variant_$NAME
 mkdir -p $OBJ $ROOT/abv
 make -s -C $CS >/dev/null
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I$ROOT/include -I$CS"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Werror=pass-failed -I$ROOT/include -I$CS"
 objs=""
 for f in gcow_kernels gcow_blocks var1d gcow_api; do
   src=$CS/$f.hip; [ -f $src ] || src=$CS/$f.cpp
