@@ -1479,10 +1479,13 @@ template <uint32_t WB, int U>
 __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
                                                            float* __restrict__ out, uint64_t base_bits)
 {
-  // (the pair table's unrolled group loop keeps this kernel's 16-block loop from being unrolled, and its counted waits
-  // need that; rolled, the pair loop was slower than the one-plane table: profiles/r04_dec_pair_table.log)
-  constexpr bool PAIR = false;
-  using Tab = DecTab1;
+  // 64-bit blocks: the two-plane table, at U = 8 (at U = 16 the unrolled pair loop keeps the block loop rolled, which
+  // its counted waits cannot take; profiles/r04_dec_pair_table.log)
+#ifndef GCOW_C2DEC_PAIR
+#define GCOW_C2DEC_PAIR 1
+#endif
+  constexpr bool PAIR = WB == 64 && GCOW_C2DEC_PAIR;
+  using Tab = typename std::conditional<PAIR, DecTabP, DecTab1>::type;
   __shared__ __attribute__((aligned(16))) uint32_t dtab32[sizeof(Tab) / 4];
   const uint16_t* dtab = (const uint16_t*)dtab32;
   constexpr uint32_t WBYTES = WB / 8;
@@ -2769,11 +2772,16 @@ hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint
 {
   const uint32_t nfull = (uint32_t)(F.n[0] / 4);
   constexpr uint32_t CH = 1u << 27;
-  for (uint32_t c0 = 0; c0 < nfull; c0 += CH) {  // one-shot grid, U = 16 words per lane
+  for (uint32_t c0 = 0; c0 < nfull; c0 += CH) {  // one-shot grid, U = 8 (64-bit blocks) / 16 (32-bit) words per lane
     const uint32_t nc = min(CH, nfull - c0);
     float* out = (float*)F.data + (size_t)c0 * 4;
     const uint64_t bb = base_bits + (uint64_t)c0 * p.maxbits;
-    if (p.maxbits == 64) k_decode_fixed1d_np<64, 16><<<(nc + 4095) / 4096, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+#ifndef GCOW_C2DEC_U
+#define GCOW_C2DEC_U 8
+#endif
+    if (p.maxbits == 64)
+      k_decode_fixed1d_np<64, GCOW_C2DEC_U><<<(nc + 256 * GCOW_C2DEC_U - 1) / (256 * GCOW_C2DEC_U), 256, 0, S(stream)>>>(
+          in, nc, p, out, bb);
     else k_decode_fixed1d_np<32, 16><<<(nc + 4095) / 4096, 256, 0, S(stream)>>>(in, nc, p, out, bb);
   }
   if (F.n[0] % 4) k_decode_tail1d<<<1, 1, 0, S(stream)>>>(F, p, in, base_bits, nfull);
