@@ -190,7 +190,8 @@ def encode(x: torch.Tensor, params: GcowParams, index_stride: int = 0, stream=No
 
 def decode(enc_or_words, shape=None, params: GcowParams | None = None, index: torch.Tensor | None = None,
            index_stride: int = 0, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
-    """zfp_decompress (libzfp 0.5.5 semantics) into an fp32 device tensor."""
+    """zfp_decompress (libzfp 0.5.5 semantics) into an fp32 device tensor, or into `out` (fp32; a 1-D out may be bf16:
+    the fp32 decode rounded to nearest even, as `.to(torch.bfloat16)`)."""
     if isinstance(enc_or_words, Encoded):
         e = enc_or_words
         words, shape, params = e.words, e.shape, e.params

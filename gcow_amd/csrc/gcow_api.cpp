@@ -76,7 +76,7 @@ gcow_status make_field(const zfp_input* in, gcow::FieldDesc& F, bool for_decode,
 
   if (for_decode) {
     if (in->dtype != dtype_float && !(bf16_out && in->dtype == dtype_bf16))
-      return fail(GCOW_ERR_UNSUPPORTED, bf16_out ? "decode_mean writes dtype_float or dtype_bf16"
+      return fail(GCOW_ERR_UNSUPPORTED, bf16_out ? "decode writes dtype_float, or dtype_bf16 for 1-D fields"
                                                  : "decode writes fp32 (dtype_float) only");
   } else if (in->dtype != dtype_float && in->dtype != dtype_bf16) {
     return fail(GCOW_ERR_UNSUPPORTED, "encode supports dtype_float and dtype_bf16");
@@ -222,8 +222,9 @@ gcow_status decode_impl(const zfp_input* field, const gcow_params* p, const void
                         size_t in_bytes = 0)
 {
   gcow::FieldDesc F;
-  gcow_status st = make_field(field, F, true);
+  gcow_status st = make_field(field, F, true, true);
   if (st) return st;
+  if (F.dtype == gcow::DT_BF16 && F.dims != 1) return fail(GCOW_ERR_UNSUPPORTED, "bf16 output is for 1-D fields");
   if ((st = check_params(p, F.dims))) return st;
   if (!d_in) return fail(GCOW_ERR_INVALID, "null input stream");
   if (F.nblocks == 0) return GCOW_OK;

@@ -213,7 +213,8 @@ __global__ __launch_bounds__(64) void k_decode(FieldDesc F, Params p, const uint
   for (; b < bend; b++) {
     float f[B];
     decode_block<D>(r, p, f);
-    scatter_block<D>(F, (uint32_t)b, f);
+    if constexpr (D == 1) store_block1d(F, b, f);  // fp32 or bf16 output
+    else scatter_block<D>(F, (uint32_t)b, f);
   }
   if (end_out && c == nchunks - 1) *end_out = r.pos;
 }

@@ -1475,9 +1475,9 @@ template <> struct PipeWord<32> {
 // One-shot fixed-rate 1-D decoder (the shape of k_encode_fixed1d_np): each lane decodes U blocks 256 apart inside
 // its workgroup's chunk; the U word loads are issued before the table fill, and block k waits for its own word only
 // (U loads then k stores outstanding: vmcnt(U - 1)).
-template <uint32_t WB, int U>
+template <uint32_t WB, int U, bool BF = false>
 __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restrict__ in, uint32_t nfull, Params p,
-                                                           float* __restrict__ out, uint64_t base_bits)
+                                                           void* __restrict__ out, uint64_t base_bits)
 {
   // 64-bit blocks: the two-plane table, at U = 8 (at U = 16 the unrolled pair loop keeps the block loop rolled, which
   // its counted waits cannot take; profiles/r04_dec_pair_table.log)
@@ -1490,7 +1490,8 @@ __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restric
   const uint16_t* dtab = (const uint16_t*)dtab32;
   constexpr uint32_t WBYTES = WB / 8;
   const pipe_v4i rin = buf_rsrc((const char*)in + base_bits / 8, nfull * WBYTES);
-  const __amdgpu_buffer_rsrc_t rout_b = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(nfull * 16u), 0x00020000);
+  // output: 16 B per block (fp32), or 8 B (BF: bf16, rounded to nearest even)
+  const __amdgpu_buffer_rsrc_t rout_b = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(nfull * (BF ? 8u : 16u)), 0x00020000);
   const uint32_t b0 = blockIdx.x * (256u * U) + threadIdx.x;
   // the 10 KiB plane table (640 16-byte chunks, 3 per lane; the range check zeroes the rest) is requested first and
   // waited for with vmcnt(U): the U word loads behind it stay in flight, and no wait counts a memory round trip per
@@ -1521,12 +1522,19 @@ __global__ __launch_bounds__(256) void k_decode_fixed1d_np(const void* __restric
       BitReader rd{(const uint64_t*)in, base_bits + (uint64_t)b * WB};
       decode_block<1>(rd, p, f);
     }
-    pipe_v4u v;
-    v.x = __float_as_uint(f[0]); v.y = __float_as_uint(f[1]); v.z = __float_as_uint(f[2]); v.w = __float_as_uint(f[3]);
-    // 16-B store through the compiler (it inserts the VALU-write -> wide-store wait states that an inline-asm store
-    // would need by hand; with an asm store lanes 12-15 of each row stored stale data). It still counts in vmcnt
+    // 16-B (8-B) store through the compiler (it inserts the VALU-write -> wide-store wait states that an inline-asm
+    // store would need by hand; with an asm store lanes 12-15 of each row stored stale data). It still counts in vmcnt
     // exactly once per block, as the hand-counted waits assume; aux 2 = non-temporal.
-    __builtin_amdgcn_raw_buffer_store_b128(v, rout_b, (int)(b * 16u), 0, 2);
+    if constexpr (BF) {
+      pipe_v2u v;
+      v.x = bf16x2_rne(f[0], f[1]);
+      v.y = bf16x2_rne(f[2], f[3]);
+      __builtin_amdgcn_raw_buffer_store_b64(v, rout_b, (int)(b * 8u), 0, 2);
+    } else {
+      pipe_v4u v;
+      v.x = __float_as_uint(f[0]); v.y = __float_as_uint(f[1]); v.z = __float_as_uint(f[2]); v.w = __float_as_uint(f[3]);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rout_b, (int)(b * 16u), 0, 2);
+    }
   }
 }
 
@@ -1653,69 +1661,22 @@ __global__ __launch_bounds__(256) void k_decode1d_var(FieldDesc F, Params p, con
     float g[16][4];
 #pragma unroll
     for (int k = 0; k < 16; k++) decode_block1d_var(GlobalWindow{in}, pos, dtab, p.minexp, p.maxprec, g[k]);
+    if (F.dtype == DT_BF16) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) *(float4*)(out + 4 * (b0 + k)) = make_float4(g[k][0], g[k][1], g[k][2], g[k][3]);
+      for (int k = 0; k < 16; k++) store_block1d(F, b0 + k, g[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++) *(float4*)(out + 4 * (b0 + k)) = make_float4(g[k][0], g[k][1], g[k][2], g[k][3]);
+    }
     if (end_out && c == nchunks - 1) *end_out = pos;
     return;
   }
   for (uint64_t b = b0; b < b1; b++) {
     float f[4];
     decode_block1d_var(GlobalWindow{in}, pos, dtab, p.minexp, p.maxprec, f);
-    if (4 * b + 4 <= F.n[0]) *(float4*)(out + 4 * b) = make_float4(f[0], f[1], f[2], f[3]);
-    else scatter_block<1>(F, (uint32_t)b, f);
+    if (F.dtype != DT_BF16 && 4 * b + 4 <= F.n[0]) *(float4*)(out + 4 * b) = make_float4(f[0], f[1], f[2], f[3]);
+    else store_block1d(F, b, f);
   }
-  if (end_out && c == nchunks - 1) *end_out = pos;
-}
-
-// The same decoder with the workgroup's stream span staged in LDS first (128 lanes x 16-block chunks: the span runs
-// from chunk c0's index entry to chunk c0 + 128's, at most 128 x 16 x 160 bits): one coalesced copy instead of each
-// lane's chain of dependent global window loads.
-// Capacity: 80 bits per block on average; a workgroup whose span is larger decodes from global memory instead.
-// Only the no-budget rows (r = 7) of the plane table are needed here: 640 entries.
-template <uint32_t LANES>
-__global__ __launch_bounds__(LANES) void k_decode1d_var_staged(FieldDesc F, Params p, const uint64_t* __restrict__ in,
-                                                               uint64_t in_words, const uint64_t* __restrict__ index,
-                                                               uint64_t nchunks, uint64_t base_bits,
-                                                               uint64_t* __restrict__ end_out)
-{
-  constexpr uint32_t CAP = LANES * 16 * 80 / 64;  // stream words the stage holds
-  __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
-  __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
-  const uint32_t tid = threadIdx.x;
-  const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
-  const uint64_t w0 = ((base_bits + index[c0]) >> 6) & ~1ull;  // 16-byte aligned start
-  const uint64_t wend = c0 + LANES < nchunks ? ((base_bits + index[c0 + LANES] + 63) >> 6) : in_words;
-  const uint64_t span = min<uint64_t>(wend, in_words) - w0;
-  const bool staged = span <= CAP;
-  const uint64_t c = c0 + tid;
-  const uint64_t mine = c < nchunks ? index[c] : 0ull;  // requested with the span, not after it
-  stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
-  // the span (and zeros after it: the windows read up to two words past a block's last bit) in one round trip
-  if (staged) stage_lds16<LANES, (CAP + 4) / 2>(sw, in + w0, (uint32_t)(8 * span));
-  __syncthreads();
-  if (c >= nchunks) return;
-  const uint64_t b0 = c * 16, b1 = min<uint64_t>(b0 + 16, F.nblocks);
-  float* out = (float*)F.data;
-  uint64_t pos = base_bits + mine;
-  auto run = [&](const auto& win, uint64_t rel) {
-    pos -= rel;
-    if (4 * b1 <= F.n[0] && b1 - b0 == 16) {
-      float g[16][4];
-#pragma unroll
-      for (int k = 0; k < 16; k++) decode_block1d_var(win, pos, dt7, p.minexp, p.maxprec, g[k]);
-#pragma unroll
-      for (int k = 0; k < 16; k++) *(float4*)(out + 4 * (b0 + k)) = make_float4(g[k][0], g[k][1], g[k][2], g[k][3]);
-    } else {
-      for (uint64_t b = b0; b < b1; b++) {
-        float f[4];
-        decode_block1d_var(win, pos, dt7, p.minexp, p.maxprec, f);
-        scatter_block<1>(F, (uint32_t)b, f);
-      }
-    }
-    pos += rel;
-  };
-  if (staged) run(LdsWindow{sw}, 64 * w0);
-  else run(GlobalWindow{in}, 0);
   if (end_out && c == nchunks - 1) *end_out = pos;
 }
 
@@ -1877,14 +1838,14 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params
       for (uint64_t b = b0; b < b1; b++) {
         float f[4];
         decode_block1d_var(LdsWindow{sw}, pos, dt7, p.minexp, p.maxprec, f);
-        scatter_block<1>(F, (uint32_t)b, f);
+        store_block1d(F, b, f);
       }
       pos += 64 * w0;
     } else {
       for (uint64_t b = b0; b < b1; b++) {
         float f[4];
         decode_block1d_var(GlobalWindow{in}, pos, dt7, p.minexp, p.maxprec, f);
-        scatter_block<1>(F, (uint32_t)b, f);
+        store_block1d(F, b, f);
       }
     }
     if (end_out && c == nchunks - 1) *end_out = pos;
@@ -1895,6 +1856,8 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params
   uint32_t pos = (uint32_t)(base_bits + mine - 64 * w0);
   const uint32_t lane = tid & 63u, m = lane & 7u;
   float4* o4 = (float4*)out + (c - m) * 16 + m;  // block m of the group's first chunk
+  uint2* o2 = (uint2*)F.data + (c - m) * 16 + m;  // bf16 output: 8 bytes per block
+  const bool bf = F.dtype == DT_BF16;
 #pragma unroll 1  // two copies of the 8-block body are past the unroller's size limit (nothing here needs them)
   for (int rnd = 0; rnd < 2; rnd++) {
     float g[8][4];
@@ -1910,8 +1873,14 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params
     xpose8_stage<1>(g, lane);
     xpose8_stage<2>(g, lane);
     xpose8_stage<4>(g, lane);
+    if (bf) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) o4[16 * i + 8 * rnd] = make_float4(g[i][0], g[i][1], g[i][2], g[i][3]);
+      for (int i = 0; i < 8; i++)
+        o2[16 * i + 8 * rnd] = make_uint2(bf16x2_rne(g[i][0], g[i][1]), bf16x2_rne(g[i][2], g[i][3]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; i++) o4[16 * i + 8 * rnd] = make_float4(g[i][0], g[i][1], g[i][2], g[i][3]);
+    }
   }
   if (end_out && c == nchunks - 1) *end_out = pos + 64 * w0;
 }
@@ -1923,7 +1892,7 @@ __global__ void k_decode_tail1d(FieldDesc F, Params p, const uint64_t* __restric
   BitReader r{in, base_bits + (uint64_t)b * p.maxbits};
   float f[4];
   decode_block<1>(r, p, f);
-  scatter_block<1>(F, b, f);
+  store_block1d(F, b, f);
 }
 
 // Many-workgroup form of k_scan_ranges for up to kScanMwMax ranges: workgroup g scans ranges [1024 g, 1024 g + 1024)
@@ -2371,7 +2340,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_
 }
 
 // Variable rate (1-D closed-form domain) with each stream's block index every 16 blocks (index_words entries apart):
-// the shape of k_decode1d_var_staged -- LANES chunks of 16 blocks per workgroup, the workgroup's span of each stream
+// the shape of k_decode1d_var_lean -- LANES chunks of 16 blocks per workgroup, the workgroup's span of each stream
 // staged in LDS in turn -- with the 16 blocks' 64 values accumulated in registers across the streams and stored once.
 template <uint32_t LANES>
 __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params p, const uint64_t* __restrict__ in,
@@ -2774,15 +2743,18 @@ hipError_t launch_decode_fixed1d(const FieldDesc& F, const Params& p, const uint
   constexpr uint32_t CH = 1u << 27;
   for (uint32_t c0 = 0; c0 < nfull; c0 += CH) {  // one-shot grid, U = 8 (64-bit blocks) / 16 (32-bit) words per lane
     const uint32_t nc = min(CH, nfull - c0);
-    float* out = (float*)F.data + (size_t)c0 * 4;
+    const bool bf = F.dtype == DT_BF16;
+    void* out = (char*)F.data + (size_t)c0 * 4 * (bf ? 2 : 4);
     const uint64_t bb = base_bits + (uint64_t)c0 * p.maxbits;
 #ifndef GCOW_C2DEC_U
 #define GCOW_C2DEC_U 8
 #endif
-    if (p.maxbits == 64)
-      k_decode_fixed1d_np<64, GCOW_C2DEC_U><<<(nc + 256 * GCOW_C2DEC_U - 1) / (256 * GCOW_C2DEC_U), 256, 0, S(stream)>>>(
-          in, nc, p, out, bb);
-    else k_decode_fixed1d_np<32, 16><<<(nc + 4095) / 4096, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+    constexpr uint32_t U64 = GCOW_C2DEC_U;
+    const uint32_t g64 = (nc + 256 * U64 - 1) / (256 * U64), g32 = (nc + 4095) / 4096;
+    if (p.maxbits == 64 && bf) k_decode_fixed1d_np<64, U64, true><<<g64, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+    else if (p.maxbits == 64) k_decode_fixed1d_np<64, U64><<<g64, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+    else if (bf) k_decode_fixed1d_np<32, 16, true><<<g32, 256, 0, S(stream)>>>(in, nc, p, out, bb);
+    else k_decode_fixed1d_np<32, 16><<<g32, 256, 0, S(stream)>>>(in, nc, p, out, bb);
   }
   if (F.n[0] % 4) k_decode_tail1d<<<1, 1, 0, S(stream)>>>(F, p, in, base_bits, nfull);
   return hipGetLastError();

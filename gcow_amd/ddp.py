@@ -125,8 +125,11 @@ def roundtrip_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.T
         # per-bucket buffers: DDP may run several buckets' callbacks before the first one's decode has read its words
         words, _, index = cdc.encode(x, state.params, stride,
                                      slot=("roundtrip", bucket.index() if hasattr(bucket, "index") else None))
-        out = cdc.decode(words, x.numel(), state.params, index=index, index_stride=stride)
-        flat.copy_(out.to(flat.dtype))
+        if flat.dtype in (torch.float32, torch.bfloat16) and flat.is_contiguous():
+            cdc.decode(words, x.numel(), state.params, index=index, index_stride=stride, out=flat)  # in place
+        else:
+            out = cdc.decode(words, x.numel(), state.params, index=index, index_stride=stride)
+            flat.copy_(out.to(flat.dtype))
         return t
 
     return fut.then(lossy)

@@ -237,7 +237,8 @@ gcow_status gcow_encode_device_append(const zfp_input* field, const gcow_params*
                                       void* hip_stream);
 
 /*
- * Decode d_in into field->data (DEVICE fp32 pointer) with libzfp 0.5.5 semantics. Fixed-rate streams
+ * Decode d_in into field->data (DEVICE fp32 pointer; for a 1-D field also dtype_bf16: the fp32 decode rounded to
+ * nearest even, torch's conversion) with libzfp 0.5.5 semantics. Fixed-rate streams
  * (minbits == maxbits) decode one block per thread; variable-rate streams need the index written by
  * gcow_encode_device (d_index/index_stride), or, with d_index == NULL, are decoded by a single sequential GPU lane.
  */

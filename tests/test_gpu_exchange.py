@@ -377,10 +377,11 @@ def test_ddp_hooks_world1_bit_exact(gc, orc, nccl_world1, hook, mode):
     assert len(set(seen)) >= 2, seen  # several buckets per step
 
 
+@pytest.mark.parametrize("hook", ["roundtrip_hook", "compressed_allgather_hook"])
 @pytest.mark.parametrize("mode", ["rate16", "acc1e-6"])
-def test_ddp_allgather_hook_bf16_world1(gc, orc, nccl_world1, mode):
-    """bf16 model over RCCL: the all-gather hook decodes and averages straight into the bf16 bucket; every weight
-    gradient equals the oracle's decode of its (exactly widened) bf16 gradient, divided by 1 and rounded to nearest
+def test_ddp_allgather_hook_bf16_world1(gc, orc, nccl_world1, mode, hook):
+    """bf16 model over RCCL: both hooks decode straight into the bf16 bucket; every weight gradient equals the
+    oracle's decode of its (exactly widened) bf16 gradient (divided by 1 for the all-gather hook), rounded to nearest
     even, bit for bit, over two steps and several buckets."""
     from gcow_amd import ddp
     params = gc.rate(16, 1) if mode == "rate16" else gc.accuracy(1e-6)
@@ -390,7 +391,7 @@ def test_ddp_allgather_hook_bf16_world1(gc, orc, nccl_world1, mode):
     model, ref = layers(), layers()
     ref.load_state_dict(model.state_dict())
     dm = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=1)
-    dm.register_comm_hook(ddp.GcowHookState(params=params), ddp.compressed_allgather_hook)
+    dm.register_comm_hook(ddp.GcowHookState(params=params), getattr(ddp, hook))
     op = orc.expert(*params.tuple())
     for step in range(2):
         model.zero_grad()
@@ -401,7 +402,7 @@ def test_ddp_allgather_hook_bf16_world1(gc, orc, nccl_world1, mode):
         for lm, lr in zip(model, ref):
             gb = lr.weight.grad.reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
             dec = orc.decompress(orc.compress(gb, op)[0], gb.shape, op)
-            want = _bf16_rne((np.zeros_like(dec) + dec) / np.float32(1))
+            want = _bf16_rne((np.zeros_like(dec) + dec) / np.float32(1) if hook == "compressed_allgather_hook" else dec)
             got = lm.weight.grad.reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
             assert np.array_equal(got, want), step
 

@@ -110,6 +110,45 @@ def test_fast1d_fixed_rate(gc, orc, n, r):
     _check_vs_oracle(gc, orc, a, orc.rate(r, 1))
 
 
+def _bf16_rne(a):
+    u = a.view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+BF16_OUT_MODES = {"rate16": ("rate", 16), "rate8": ("rate", 8), "rate12": ("rate", 12), "acc1e-6": ("acc", 1e-6),
+                  "acc1e-3": ("acc", 1e-3), "expert_trunc": ("expert", (1, 100, 64, -30))}
+
+
+@pytest.mark.parametrize("mode", list(BF16_OUT_MODES))
+@pytest.mark.parametrize("layout", ["contiguous", "strided"])
+@pytest.mark.parametrize("n", [4 * 128 * 16 * 3 + 4 * 37 + 3, 4 * 20001])
+def test_decode_1d_bf16_output(gc, orc, mode, layout, n):
+    """1-D decode into a bf16 tensor: the oracle's fp32 decode rounded to nearest even, bit for bit -- the fixed-rate
+    one-shot decoders (64- and 32-bit blocks), the lean variable-rate decoder (whole workgroups) with its general path
+    (the partial chunk), the generic decoder, the partial last block, and a strided output (value stores)."""
+    kind, v = BF16_OUT_MODES[mode]
+    op = orc.rate(v, 1) if kind == "rate" else orc.accuracy(v) if kind == "acc" else orc.expert(*v)
+    a = orc.gen_normal(n, 1e-3, 0xB16 + n, True)
+    fixed = op.minbits == op.maxbits
+    e, _ = dev_encode_bytes(gc, a, P(gc, op), 0 if fixed else 16)
+    base = torch.full((2 * n,), -1.0, dtype=torch.bfloat16, device="cuda")
+    out = base[:n] if layout == "contiguous" else base[::2]
+    got = gc.decode(e, out=out)
+    want = _bf16_rne(orc.decompress(orc.compress(a, op)[0], a.shape, op))
+    torch.cuda.synchronize()
+    assert got.data_ptr() == out.data_ptr()
+    assert np.array_equal(got.cpu().view(torch.int16).numpy().view(np.uint16), want)
+    untouched = base[n:] if layout == "contiguous" else base[1::2]
+    assert bool((untouched == -1.0).all())
+
+
+def test_decode_bf16_output_needs_1d(gc, orc):
+    a = orc.gen_normal(16 * 16, 1e-3, 5, False).reshape(16, 16)
+    e, _ = dev_encode_bytes(gc, a, gc.rate(16, 2))
+    with pytest.raises(gc.GcowError):
+        gc.decode(e, out=torch.empty((16, 16), dtype=torch.bfloat16, device="cuda"))
+
+
 @pytest.mark.parametrize("r", [4, 2.5, 32, 12])
 def test_1d_other_rates(gc, orc, r):
     a = orc.gen_normal(10007, 1e-3, 99, True)
@@ -782,7 +821,7 @@ def test_var1d_mixed_tile_sizes(gc, orc, dtype, appended):
 def test_c5_full_size_accuracy(gc, orc, dtype, tol):
     """BASELINE config 5 shape (bf16) and its fp32 twin: 256 Mi values of the bench's bucket (bf16 by exact
     widening), accuracy 1e-6 and 1e-3 (both timed by bench.py), stream vs the threaded oracle, and the whole
-    variable-rate decode (k_decode1d_var_staged, the receive side of the DDP hook) vs the threaded oracle decode."""
+    variable-rate decode (k_decode1d_var_lean, the receive side of the DDP hook) vs the threaded oracle decode."""
     n = 256 * 1024 * 1024
     T = min(16, os.cpu_count() or 1)
     x = torch.empty(n, dtype=torch.float32, device="cuda")
