@@ -474,10 +474,16 @@ def leg_configs(ctx):
         _, dper = timed(ctx, lambda: codec.decode(e, out=back, stream=st), 5, 20, stream=st)
         dk = sum(dper) / len(dper)
         dr = roof(cbits / 8, n * 4, dk, "k_decode1d_var_lean<128>", basis="write")
+        # the same decode into a bf16 tensor (the bf16 bucket's own dtype: rounded to nearest even in the store)
+        back_b = torch.empty(n, dtype=torch.bfloat16, device=ctx.dev)
+        _, bper = timed(ctx, lambda: codec.decode(e, out=back_b, stream=st), 5, 20, stream=st)
+        bk = sum(bper) / len(bper)
+        del back_b
         out[name] = {"encode_ms": round(k_ms, 4), "encode_GiBps_input": round(gib(n * 2, k_ms), 2),
                      "bits_per_value": round(cbits / n, 3), "encode_roofline": er,
                      "decode_ms": round(dk, 4), "decode_GiBps_output": round(gib(n * 4, dk), 2),
                      "decode_roofline": dr,
+                     "decode_bf16_out_ms": round(bk, 4), "decode_bf16_out_GiBps_output": round(gib(n * 2, bk), 2),
                      "host_path_ms": round(h_ms, 3), "host_path_GiBps_input": round(gib(n * 2, h_ms), 2),
                      "host_path_note": "pinned bf16 H2D + encode + D2H of the stream, 16 overlapped chunks (PCIe-bound: at 1e-6 the stream is as large as the bf16 input, so the D2H leg binds as much as the H2D; profiles/r04_host_chunks.log)"}
         del enc, h_in, h_out, henc, e, back
