@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
@@ -1804,27 +1805,50 @@ __device__ __forceinline__ void xpose8_stage(float (&g)[8][4], uint32_t lane)
 // profiles/r04_var_decode_occupancy_ab.log). A workgroup whose span does not fit (a higher rate), partial chunks and
 // strided outputs take the general path (global-memory windows; staging such a workgroup in 2 or 4 parts instead
 // measured slower on the common path, profiles/r04_var_decode_parts_negative.log).
-template <uint32_t LANES>
-__global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params p, const uint64_t* __restrict__ in,
-                                                             uint64_t in_words, const uint64_t* __restrict__ index,
-                                                             uint64_t nchunks, uint64_t base_bits,
-                                                             uint64_t* __restrict__ end_out)
-{
 #ifndef GCOW_VDEC_CAPB
 #define GCOW_VDEC_CAPB 64
 #endif
-  constexpr uint32_t CAP = LANES * 16 * GCOW_VDEC_CAPB / 64;  // stream words the stage holds (64 bits per block)
-  __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
-  __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
+#ifndef GCOW_VDEC_BIGB
+#define GCOW_VDEC_BIGB 144
+#endif
+// Stage capacity in stream words: the main kernel's (GCOW_VDEC_CAPB bits per block on average) and the second pass's
+// (any span: a 1-D block codes at most 140 bits, plus the 16-byte alignment of the span's start)
+template <uint32_t LANES> constexpr uint32_t vdec_cap() { return LANES * 16 * GCOW_VDEC_CAPB / 64; }
+template <uint32_t LANES> constexpr uint32_t vdec_cap_big() { return LANES * 16 * GCOW_VDEC_BIGB / 64; }
+
+// A group of LANES index chunks (one workgroup's work) whose span does not fit the main kernel's stage, and which is
+// whole (no partial chunk or block) with a contiguous output: left by the main kernel to k_decode1d_var_lean_big.
+// Not the last group: its span ends at the stream's end, which the index does not give (the buffer's end bounds it),
+// so it takes the main kernel's general path.
+template <uint32_t LANES>
+__device__ __forceinline__ bool vdec_left_to_big(const FieldDesc& F, const uint64_t* index, uint64_t in_words,
+                                                 uint64_t nchunks, uint64_t base_bits, uint64_t c0)
+{
+  const bool whole = c0 + LANES < nchunks && 16 * (c0 + LANES) <= (uint64_t)F.n[0] / 4;
+  if (!whole || !F.vec) return false;
+  const uint64_t w0 = ((base_bits + index[c0]) >> 6) & ~1ull;
+  const uint64_t wend = (base_bits + index[c0 + LANES] + 63) >> 6;
+  return min<uint64_t>(wend, in_words) - w0 > vdec_cap<LANES>();
+}
+
+// One group: its span staged in sw (CAP words), each lane's 16 blocks decoded by the lean block decoder, stored
+// through the 8 x 8 lane transposes. BIG: the second pass (stage the caller's sw only after a barrier: the previous
+// group's readers are done); else the main kernel, which stages dt7 with the span in one round trip.
+template <uint32_t LANES, uint32_t CAP, bool BIG>
+__device__ __forceinline__ void vdec_group(const FieldDesc& F, const Params& p, const uint64_t* __restrict__ in,
+                                           uint64_t in_words, const uint64_t* __restrict__ index, uint64_t nchunks,
+                                           uint64_t base_bits, uint64_t* __restrict__ end_out, uint64_t c0,
+                                           uint16_t* dt7, uint64_t* sw)
+{
   const uint32_t tid = threadIdx.x;
-  const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
   const uint64_t w0 = ((base_bits + index[c0]) >> 6) & ~1ull;  // 16-byte aligned start
   const uint64_t wend = c0 + LANES < nchunks ? ((base_bits + index[c0 + LANES] + 63) >> 6) : in_words;
   const uint64_t span = min<uint64_t>(wend, in_words) - w0;
   const bool staged = span <= CAP;
   const uint64_t c = c0 + tid;
   const uint64_t mine = c < nchunks ? index[c] : 0ull;
-  stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
+  if constexpr (BIG) __syncthreads();
+  else stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
   if (staged) stage_lds16<LANES, (CAP + 4) / 2>(sw, in + w0, (uint32_t)(8 * span));
   __syncthreads();
   float* out = (float*)F.data;
@@ -1883,6 +1907,68 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params
     }
   }
   if (end_out && c == nchunks - 1) *end_out = pos + 64 * w0;
+}
+
+template <uint32_t LANES>
+__global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                             uint64_t in_words, const uint64_t* __restrict__ index,
+                                                             uint64_t nchunks, uint64_t base_bits,
+                                                             uint64_t* __restrict__ end_out, uint64_t* __restrict__ left,
+                                                             uint64_t seq)
+{
+  __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
+  __shared__ __attribute__((aligned(16))) uint64_t sw[vdec_cap<LANES>() + 4];
+  const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
+  if (vdec_left_to_big<LANES>(F, index, in_words, nchunks, base_bits, c0)) {  // workgroup-uniform
+    if (left && threadIdx.x == 0) *left = seq;  // the second pass has work (every such workgroup stores the same value)
+    return;
+  }
+  vdec_group<LANES, vdec_cap<LANES>(), false>(F, p, in, in_words, index, nchunks, base_bits, end_out, c0, dt7, sw);
+}
+
+template <uint32_t LANES>
+__device__ __forceinline__ void vdec_group_big(const FieldDesc& F, const Params& p, const uint64_t* __restrict__ in,
+                                            uint64_t in_words, const uint64_t* __restrict__ index, uint64_t nchunks,
+                                            uint64_t base_bits, uint64_t* __restrict__ end_out, uint64_t c0,
+                                            uint16_t* dt7, uint64_t* sw)
+{
+  vdec_group<LANES, vdec_cap_big<LANES>(), true>(F, p, in, in_words, index, nchunks, base_bits, end_out, c0, dt7, sw);
+}
+
+template <uint32_t LANES>
+__global__ __launch_bounds__(LANES) void k_decode1d_var_lean_big(FieldDesc F, Params p, const uint64_t* __restrict__ in,
+                                                                 uint64_t in_words, const uint64_t* __restrict__ index,
+                                                                 uint64_t nchunks, uint64_t base_bits,
+                                                                 uint64_t* __restrict__ end_out,
+                                                                 const uint64_t* __restrict__ left, uint64_t seq)
+{
+  __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
+  __shared__ __attribute__((aligned(16))) uint64_t sw[vdec_cap_big<LANES>() + 4];
+  __shared__ uint32_t todo[LANES];
+  __shared__ uint32_t ntodo;
+  if (left && *left != seq) return;  // the main kernel left nothing (no flag buffer: check every group)
+  const uint64_t ng = (nchunks + LANES - 1) / LANES;
+  bool staged_tab = false;
+  // sweep k: workgroup w checks groups k G LANES + t G + w (t < LANES, G = gridDim.x): the groups spread over every
+  // workgroup of the grid
+  const uint64_t G = gridDim.x;
+  for (uint64_t gb = 0; gb < ng; gb += G * LANES) {
+    if (threadIdx.x == 0) ntodo = 0;
+    __syncthreads();
+    const uint64_t g = gb + (uint64_t)threadIdx.x * G + blockIdx.x;
+    if (g < ng && vdec_left_to_big<LANES>(F, index, in_words, nchunks, base_bits, g * LANES))
+      todo[atomicAdd(&ntodo, 1u)] = threadIdx.x;
+    __syncthreads();
+    const uint32_t nt = ntodo;
+    if (nt && !staged_tab) {  // the decode table only once there is work
+      stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
+      staged_tab = true;
+    }
+    for (uint32_t i = 0; i < nt; i++)
+      vdec_group_big<LANES>(F, p, in, in_words, index, nchunks, base_bits, end_out,
+                            (gb + (uint64_t)todo[i] * G + blockIdx.x) * LANES, dt7, sw);
+    __syncthreads();  // todo / ntodo are rewritten next sweep
+  }
 }
 
 // the partial last block of a 1-D field (generic decoder, one lane)
@@ -2727,8 +2813,24 @@ hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64
 {
   if (index && chunk == 16 && in_words) {  // the workgroup's stream span staged in LDS, 128 lanes
     constexpr uint32_t L = 128;
-    k_decode1d_var_lean<L><<<(uint32_t)((nchunks + L - 1) / L), L, 0, S(stream)>>>(F, p, in, in_words, index, nchunks,
-                                                                                  base_bits, end_out);
+    const uint64_t ng = (nchunks + L - 1) / L;
+    // a stream-ordered flag word (its own allocation per call: decodes on other streams do not share it), set to this
+    // call's sequence number by a main-kernel workgroup that leaves its group to the second pass, so an empty second
+    // pass costs one load per workgroup instead of every group's span check (~40 us). Not initialised: a stale word
+    // equal to seq (a number no earlier call used) would only make the second pass check every group.
+    static std::atomic<uint64_t> g_seq{0x67636f77ull << 32};
+    const uint64_t seq = ++g_seq;
+    hipStream_t st = S(stream);
+    uint64_t* left = nullptr;
+    if (hipMallocAsync((void**)&left, sizeof(uint64_t), st) != hipSuccess) {
+      (void)hipGetLastError();
+      left = nullptr;
+    }
+    k_decode1d_var_lean<L><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left,
+                                                       seq);
+    const uint32_t gbig = (uint32_t)std::min<uint64_t>(ng, 1024);
+    k_decode1d_var_lean_big<L><<<gbig, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left, seq);
+    if (left) (void)hipFreeAsync(left, st);
     return hipGetLastError();
   }
   k_decode1d_var<<<(uint32_t)((nchunks + 255) / 256), 256, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, base_bits,

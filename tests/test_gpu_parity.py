@@ -142,6 +142,28 @@ def test_decode_1d_bf16_output(gc, orc, mode, layout, n):
     assert bool((untouched == -1.0).all())
 
 
+@pytest.mark.parametrize("tol", [2e-7, 1e-8, 1e-12])
+@pytest.mark.parametrize("out_dtype", ["f32", "bf16"])
+def test_var1d_decode_past_the_stage(gc, orc, tol, out_dtype):
+    """1-D variable-rate streams coding more than the lean decoder's 64-bit-per-block stage (75-140 bits per block):
+    the main kernel leaves those groups to the second pass (a stage that holds any span); whole groups, a partial last
+    group and a partial last block, bit for bit against the oracle."""
+    n = 4 * 16 * 128 * 5 + 4 * 16 * 37 + 4 * 5 + 2
+    op = orc.accuracy(tol)
+    a = orc.gen_normal(n, 1e-3, 0x51A6E, True)
+    e, _ = dev_encode_bytes(gc, a, P(gc, op), 16)
+    assert e.bits / ((n + 3) // 4) > 64
+    ref = orc.decompress(orc.compress(a, op)[0], a.shape, op)
+    if out_dtype == "f32":
+        got = gc.decode(e)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    else:
+        got = gc.decode(e, out=torch.empty(n, dtype=torch.bfloat16, device="cuda"))
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().view(torch.int16).numpy().view(np.uint16), _bf16_rne(ref))
+
+
 def test_decode_bf16_output_needs_1d(gc, orc):
     a = orc.gen_normal(16 * 16, 1e-3, 5, False).reshape(16, 16)
     e, _ = dev_encode_bytes(gc, a, gc.rate(16, 2))
