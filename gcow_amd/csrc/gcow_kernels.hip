@@ -2924,9 +2924,9 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
 #ifndef GCOW_DMEAN_LEAN
 #define GCOW_DMEAN_LEAN 1
 #endif
-    if (GCOW_DMEAN_LEAN && lean && nfull && F.nblocks < (1u << 27)) {  // one-shot grid, U = 4 per lane
+    if (GCOW_DMEAN_LEAN && lean && nfull && F.nblocks < (1u << 27)) {  // one-shot grid, U = 2 per lane (U = 1 / 4 / 8: 2.47 / 2.37 / 3.0 against 2.33 ms, W = 8 rate 16: profiles/r04_decode_mean_blocks_per_lane.log)
 #ifndef GCOW_DMEAN_U
-#define GCOW_DMEAN_U 4
+#define GCOW_DMEAN_U 2
 #endif
 #ifndef GCOW_DMEAN_D
 #define GCOW_DMEAN_D 1
