@@ -388,10 +388,33 @@ def leg_host_e2e(ctx, enc, x, p, n, in_bytes, out_bytes):
     h_ms, _ = timed(ctx, seq, 2, 5)
     henc = codec.HostEncoder(n, torch.float32, p, chunks=16, device=ctx.dev)
     o_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 2, 5)
+    ok = host_stream_check(henc, h_in, h_out, p)
     return {"ms_per_step": round(h_ms, 3), "GiBps_input": round(gib(in_bytes, h_ms), 2),
             "overlapped_ms_per_step": round(o_ms, 3), "overlapped_GiBps_input": round(gib(in_bytes, o_ms), 2),
-            "note": "pinned hipMemcpyAsync H2D + encode + D2H, PCIe-inclusive (not `value`); overlapped = 16 chunks, "
-                    "H2D / encode / D2H on three streams (codec.HostEncoder)"}
+            "host_stream_matches_oracle": ok,
+            "note": "pinned H2D + encode + D2H, PCIe-inclusive (not `value`); overlapped: 16 chunks on 3 streams"}
+
+
+def oracle_threads() -> int:
+    """Threads for the oracle checks and the multi-thread CPU legs: the CPUs this process may actually use, i.e.
+    min(sched_getaffinity, the cgroup's CPU quota) -- not the host's CPU count."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    q = _cpu_quota()
+    return max(1, min(aff, int(q)) if q else aff)
+
+
+def host_stream_check(henc, h_in: torch.Tensor, h_out: torch.Tensor, p) -> bool:
+    """One more HostEncoder call (the timed object, 16 chunks) into a zeroed pinned buffer; the WHOLE host-resident
+    stream is compared with the threaded oracle's encode of the same host bucket (every chunk seam included)."""
+    import numpy as np
+
+    from oracle import oracle as O
+    h_out.zero_()
+    bits = henc(h_in, h_out)
+    a = h_in.numpy() if h_in.dtype == torch.float32 else h_in.view(torch.int16).numpy().view(np.uint16)
+    w, b = O.compress(a, O.expert(*p.tuple()), threads=oracle_threads())
+    nw = (b + 63) // 64
+    return bool(bits == b and np.array_equal(h_out[:nw].numpy().view(np.uint64), w[:nw]))
 
 
 def leg_configs(ctx):
@@ -461,6 +484,7 @@ def leg_configs(ctx):
                             pin_memory=True)
         henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=16, device=ctx.dev)
         h_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 2, 5)
+        h_ok = host_stream_check(henc, h_in, h_out, p)
         er = roof(n * 2, cbits / 8, k_ms,
                   "k_count1d_var_tile + k_scan_ranges_mw + k_encode1d_var_tile (+ k_encode1d_var_tile_big)")
         # HBM bytes of one encode (all four kernels) from a committed PMC pass (tools/c5_traffic.py); the input is read
@@ -485,7 +509,8 @@ def leg_configs(ctx):
                      "decode_roofline": dr,
                      "decode_bf16_out_ms": round(bk, 4), "decode_bf16_out_GiBps_output": round(gib(n * 2, bk), 2),
                      "host_path_ms": round(h_ms, 3), "host_path_GiBps_input": round(gib(n * 2, h_ms), 2),
-                     "host_path_note": "pinned bf16 H2D + encode + D2H of the stream, 16 overlapped chunks (PCIe-bound: at 1e-6 the stream is as large as the bf16 input, so the D2H leg binds as much as the H2D; profiles/r04_host_chunks.log)"}
+                     "host_path_stream_matches_oracle": h_ok,
+                     "host_path_note": "pinned bf16 H2D + encode + D2H, 16 overlapped chunks (PCIe-bound)"}
         del enc, h_in, h_out, henc, e, back
     del xb
     torch.cuda.empty_cache()
@@ -580,12 +605,14 @@ def cpu_baseline(x: torch.Tensor, rate: float, dev) -> dict:
                        16384 x 16384, fixed rate `rate` (2-D minbits = maxbits = 16 rate);
       port_1t          the oracle restatement (gcc -O3 -march=native, built here) on the C2 config (1-D rate `rate`),
                        1 thread, the bucket's first 32 Mi values;
-      port_mt          the same on the whole bucket with T = len(sched_getaffinity) threads over block-aligned shards +
-                       a serial bit stitch (port_mt_omp: T = OMP_NUM_THREADS, the box's CPU share);
+      port_mt          the same on the whole bucket with T = min(sched_getaffinity, cgroup CPU quota) threads (the
+                       CPUs this process can use; `cores` = T) over block-aligned shards + a serial bit stitch;
       c3_*, c5_*       the restatement on the C3 field (512^3, 3-D rate 8 / accuracy 1e-3; the sw/ reference has no
                        3-D) and the C5 bucket (256 Mi bf16, accuracy 1e-6; no bf16 in sw/): T threads on the whole
                        input, 1 thread on a bounded slice.
-    The headline is `reference`; without oracle/_ref it is port_1t and `reference_missing` says why."""
+    The headline is `reference`; without oracle/_ref it is port_1t and `reference_missing` says why. Every leg is also
+    reported as flat `<leg>_GiBps` / `<leg>_cores` scalars (the driver's record keeps scalars, not nested objects);
+    the long descriptions go to the top-level `cpu_baseline_legs`."""
     import ctypes as C
 
     import numpy as np
@@ -608,7 +635,7 @@ def cpu_baseline(x: torch.Tensor, rate: float, dev) -> dict:
                       "seconds_best": round(dt, 4), "best_of": reps, "sample": sample}
 
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    omp = int(os.environ.get("OMP_NUM_THREADS") or 0) or None
+    T = oracle_threads()
     R = O.ref()
     missing = None
     if R is not None:
@@ -619,50 +646,48 @@ def cpu_baseline(x: torch.Tensor, rate: float, dev) -> dict:
         out = np.zeros(O.max_words(a2.shape, p) + 4, np.uint64)
         dt = best(lambda: R.gcow_ref_compress_2d(a2.ctypes.data_as(C.POINTER(C.c_float)), side, side, *p.tuple(),
                                                    out.ctypes.data_as(C.POINTER(C.c_uint64)), out.nbytes), 3)
-        leg("reference", a2.nbytes, dt, 1, "sw/ zfp_compress on the whole 256 Mi-value bucket viewed as 16384 x 16384 "
-            "fp32, fixed rate %g (2-D: minbits = maxbits = %d), 1 thread" % (rate, p.maxbits), 3)
+        leg("reference", a2.nbytes, dt, 1, "sw/ zfp_compress, whole bucket as 16384^2 fp32 (2-D), rate %g, 1 thread"
+            % rate, 3)
         del out
     else:
-        missing = ("oracle/_ref/libgcow_ref.so absent: it is compiled from /root/reference/sw/src by oracle/Makefile "
-                   "(make -C oracle ref) in the build container and travels with the tree")
+        missing = "oracle/_ref/libgcow_ref.so absent (built from /root/reference/sw/src by oracle/Makefile)"
         print("bench.py: WARNING: " + missing, file=sys.stderr)
     L, flags = O.native_lib()
     p1 = O.rate(rate, 1)
     s1 = np.ascontiguousarray(a[: 32 << 20])
     leg("port_1t", s1.nbytes, best(lambda: O.compress(s1, p1, L=L), 5), 1,
-        "oracle restatement (%s), 1-D fixed rate %g, first 32 Mi values" % (flags, rate), 5)
-    leg("port_mt", a.nbytes, best(lambda: O.compress(a, p1, threads=aff, L=L), 5), aff,
-        "oracle restatement (%s), 1-D fixed rate %g, whole 256 Mi bucket, %d threads (sched_getaffinity) over "
-        "block-aligned shards + serial bit stitch" % (flags, rate, aff), 5)
-    if omp and omp != aff:
-        leg("port_mt_omp", a.nbytes, best(lambda: O.compress(a, p1, threads=omp, L=L), 5), omp,
-            "as port_mt with T = OMP_NUM_THREADS = %d (the box's CPU share)" % omp, 5)
+        "oracle restatement (%s), 1-D rate %g, first 32 Mi values, 1 thread" % (flags, rate), 5)
+    leg("port_mt", a.nbytes, best(lambda: O.compress(a, p1, threads=T, L=L), 5), T,
+        "oracle restatement, 1-D rate %g, whole 256 Mi bucket, %d threads (= usable CPUs)" % (rate, T), 5)
     del s1
     # C3: the 512^3 field the GPU configs leg times
     f = codec.c3_field(dev).cpu().numpy()
     slab = np.ascontiguousarray(f[:64])
     for name, op in (("c3_rate8", O.rate(8, 3)), ("c3_acc1e-3", O.accuracy(1e-3))):
-        leg(name + "_port_mt", f.nbytes, best(lambda: O.compress(f, op, threads=aff, L=L), 3), aff,
-            "oracle restatement, 3-D %s, the whole 512^3 C3 field, %d threads" % (name[3:], aff), 3)
+        leg(name + "_port_mt", f.nbytes, best(lambda: O.compress(f, op, threads=T, L=L), 3), T,
+            "oracle restatement, 3-D %s, whole 512^3 C3 field, %d threads" % (name[3:], T), 3)
         leg(name + "_port_1t", slab.nbytes, best(lambda: O.compress(slab, op, L=L), 3), 1,
-            "oracle restatement, 3-D %s, 64 z-planes (512 x 512 x 64) of the C3 field, 1 thread" % name[3:], 3)
+            "oracle restatement, 3-D %s, 512 x 512 x 64 of the C3 field, 1 thread" % name[3:], 3)
     del f, slab
     # C5: the bf16 bucket (exact widening, accuracy 1e-6)
     hb = x.to(torch.bfloat16).cpu().view(torch.int16).numpy().view(np.uint16)
     op = O.accuracy(1e-6)
-    leg("c5_bf16_acc1e-6_port_mt", hb.nbytes, best(lambda: O.compress(hb, op, threads=aff, L=L), 3), aff,
-        "oracle restatement, 1-D bf16 accuracy 1e-6, the whole 256 Mi-value C5 bucket, %d threads" % aff, 3)
+    leg("c5_bf16_acc1e-6_port_mt", hb.nbytes, best(lambda: O.compress(hb, op, threads=T, L=L), 3), T,
+        "oracle restatement, 1-D bf16 accuracy 1e-6, whole 256 Mi C5 bucket, %d threads" % T, 3)
     h1 = np.ascontiguousarray(hb[: 32 << 20])
     leg("c5_bf16_acc1e-6_port_1t", h1.nbytes, best(lambda: O.compress(h1, op, L=L), 3), 1,
-        "oracle restatement, 1-D bf16 accuracy 1e-6, first 32 Mi values of the C5 bucket, 1 thread", 3)
+        "oracle restatement, 1-D bf16 accuracy 1e-6, first 32 Mi values, 1 thread", 3)
     head = legs.get("reference") or legs["port_1t"]
     d = {"value": head["value"], "unit": "GiB/s", "cores": head["cores"],
          "kind": "reference" if "reference" in legs else "port", "sample": head["sample"],
-         "cpu": _cpu_model(), "host_cpus": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": omp,
-         "cgroup_cpu_quota": _cpu_quota(), "legs": legs}
+         "cpu": _cpu_model()[:60], "host_cpus": os.cpu_count(), "affinity_cpus": aff,
+         "cgroup_cpu_quota": _cpu_quota(), "usable_cpus": T}
+    for k, v in legs.items():
+        d[k + "_GiBps"] = v["value"]
+        d[k + "_cores"] = v["cores"]
     if missing:
         d["reference_missing"] = missing
-    return d
+    return d, legs
 
 
 # ------------------------------------------------------------------------------------------------------ main
@@ -741,8 +766,8 @@ def worker(args):
     roofline = roof(in_bytes, out_bytes, kern_ms, kname)
     traffic, src = load_pmc_traffic(kname, workload)
     roofline["traffic"] = traffic
-    roofline["traffic_source"] = (src + " (rocprofv3 --pmc TCC read + write bytes per launch, same kernel and "
-                                  "workload; not measured in this run)") if src else None
+    # committed rocprofv3 --pmc pass (FETCH_SIZE + WRITE_SIZE per launch of this kernel and workload); not this run
+    roofline["traffic_source"] = src
     if p.maxbits in (32, 64):
         # measured device-copy ceiling of the encoder's own access pattern (BASELINE.md:59): the same grid, loads and
         # stores without the coding (k_copy_pattern1d), same protocol, right after the headline
@@ -750,14 +775,12 @@ def worker(args):
         _, cper = timed(ctx, lambda: codec.copy_pattern(x, cp_out, p.maxbits, stream), args.warmup, args.steps,
                         stream=stream)
         ck = ctx.max_over_ranks([sum(cper) / len(cper)])[0]
-        roofline["copy_ceiling"] = {
-            "kernel": "k_copy_pattern1d", "kernel_ms": round(ck, 5),
-            "achieved": round(in_bytes / (ck / 1e3) / 1e9, 1), "unit": "GB/s (uncompressed bytes read)",
-            "frac": round(in_bytes / (ck / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-            "frac_read_write": round((in_bytes + out_bytes) / (ck / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-            "encoder_frac_of_ceiling": round(ck / kern_ms, 4),
-            "note": "the encoder's grid, 16-B loads and %d-bit stores per block with no coding: the HBM floor of "
-                    "this access pattern (--warmup/--steps as the headline)" % p.maxbits}
+        # flat scalars (the driver's record keeps scalar fields of `roofline`, not nested objects)
+        roofline["copy_ceiling_kernel"] = "k_copy_pattern1d"
+        roofline["copy_ceiling_ms"] = round(ck, 5)
+        roofline["copy_ceiling_frac"] = round(in_bytes / (ck / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+        roofline["copy_ceiling_frac_read_write"] = round((in_bytes + out_bytes) / (ck / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+        roofline["kernel_over_copy_ceiling"] = round(kern_ms / ck, 4)
         del cp_out
     extra = {"per_launch_ms": {"first": round(per[0], 4), "median": round(statistics.median(per), 4),
                                "min": round(min(per), 4), "max": round(max(per), 4)}}
@@ -794,7 +817,7 @@ def worker(args):
             if "x" not in locals():
                 x = torch.empty(n, dtype=torch.float32, device=ctx.dev)
                 codec.fill_normal(x, 1e-3, seed=SEED, inject=True)
-            cpu = cpu_baseline(x, args.rate, ctx.dev)
+            cpu, extra["cpu_baseline_legs"] = cpu_baseline(x, args.rate, ctx.dev)
         except Exception as ex:  # the GPU measurement stands on its own
             cpu = {"error": repr(ex)}
             print("bench.py: cpu_baseline failed: %r" % (ex,), file=sys.stderr)

@@ -864,6 +864,43 @@ def test_c5_full_size_accuracy(gc, orc, dtype, tol):
     assert np.array_equal(d.view(np.uint32), ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("case", ["c5_bf16_acc1e-6", "c5_bf16_acc1e-3", "c2_f32_rate16"])
+def test_host_encoder_full_size(gc, orc, case):
+    """The host-resident paths bench.py times, at the benched size and chunking: HostEncoder(chunks=16) on the full
+    256 Mi-value bucket (C5: bf16 by exact widening, accuracy 1e-6 / 1e-3 -- BASELINE configs[4]'s timed region is
+    pinned H2D + encode + D2H; C2: fp32 rate 16, the host_e2e leg). The whole host-resident stream, every one of the
+    16 chunk seams included, vs the threaded oracle (caller contract: hw/models/train_imagenet.py:453,471)."""
+    n = 256 * 1024 * 1024
+    T = min(16, os.cpu_count() or 1)
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    gc.fill_normal(x, 1e-3, seed=0x67636F77, inject=True)
+    if case.startswith("c5"):
+        dtype, op = torch.bfloat16, orc.accuracy(1e-6 if case.endswith("1e-6") else 1e-3)
+        h = x.to(torch.bfloat16).cpu()
+        a = h.view(torch.int16).numpy().view(np.uint16)
+    else:
+        dtype, op = torch.float32, orc.rate(16, 1)
+        h = x.cpu()
+        a = h.numpy()
+    del x
+    h = h.pin_memory()
+    params = P(gc, op)
+    enc = gc.HostEncoder(n, dtype, params, chunks=16)
+    assert len(enc.bounds) == 16
+    out = torch.zeros(gc.max_output_bytes((n,), params, dtype) // 8 + 2, dtype=torch.int64).pin_memory()
+    bits = enc(h, out)
+    w_ref, bits_ref = orc.compress(a, op, threads=T)
+    assert bits == bits_ref
+    nw = (bits + 63) // 64
+    got = out[:nw].numpy().view(np.uint64)
+    if not np.array_equal(got, w_ref):
+        bad = int(np.flatnonzero(got != w_ref)[0])
+        seams = [lo for lo, _ in enc.bounds]
+        pytest.fail("first differing word %d (bit %d); chunk starts (values) %s" % (bad, 64 * bad, seams))
+    # the words past the stream stay untouched (no stray D2H past the flushed end)
+    assert not out[nw:].any()
+
+
 def test_var1d_more_than_64ki_tiles(gc, orc):
     """Past 64 Ki tiles of 1024 blocks (256 Mi values) the range scan of the 1-D variable-rate encoder relies on the
     count's 8-tile group totals (k_scan_ranges_mw with gsums); a ragged bucket just past that size, accuracy 1e-6 on
