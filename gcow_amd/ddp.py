@@ -12,7 +12,8 @@ PCIe copies per step. Two device-resident replacements:
   (gcow_decode_mean_device: acc = 0 + x_0 + x_1 + ... in rank order, then / world). At rate r the wire carries r/32
   of the fp32 bytes per rank.
 
-Both register with `ddp_model.register_comm_hook(GcowHookState(...), hook)`. `GcowHookState.codec` defaults to the
+Both register with `ddp_model.register_comm_hook(make_hook_state(...), hook)` (variable rate: the state's exchange
+group is created by `GcowHookState.setup()`, a collective every rank calls at the same point). `GcowHookState.codec` defaults to the
 device codec (gcow_amd.dist.DeviceCodec); tests inject an oracle-backed codec to run the hook bodies over gloo.
 """
 import contextlib
@@ -33,9 +34,16 @@ INDEX_STRIDE = 16  # block index spacing the multi-stream decoder reads (one ent
 
 @dataclass
 class GcowHookState:
-    """Hook state, one per DDP model. `timeout_s` bounds every collective of the variable-rate exchange (its own
-    process group, created at the first variable-rate hook call by every member rank): a rank that fails mid-exchange
-    aborts that group, and its peers fail within the timeout instead of hanging in a collective."""
+    """Hook state, one per DDP model. `timeout_s` bounds every collective of the variable-rate exchange, which runs
+    over a process group of its own. That group is created by `setup()` -- a collective: call it on every rank of
+    `process_group`, at the same point of each rank's setup, after init_process_group and before the first backward
+    (or build the state with `make_hook_state`, which does). Constructing, copying or `dataclasses.replace`-ing a
+    state issues no collective.
+
+    Failure: a rank whose exchange raises stops its comm thread (that bucket's future and every later one fail at
+    once) and aborts the exchange group. Over gloo that closes the connections and peers blocked in an exchange
+    collective error out at once; over RCCL/NCCL a peer already blocked in a collective only fails when `timeout_s`
+    expires (the communicator's watchdog then tears the process group -- and by default the process -- down)."""
     params: GcowParams = field(default_factory=lambda: _codec.rate(16, 1))
     process_group: object = None
     codec: object = None  # None: gcow_amd.dist.device_codec()
@@ -52,24 +60,28 @@ class GcowHookState:
             self._worker = _CommWorker(self._abort_comm_group)
         return self._worker
 
-    def __post_init__(self):
-        # the exchange group is created here when possible: every rank builds its hook state at the same point of
-        # its setup, in the same order, so group creation needs no care later (creating it inside the hook would
-        # block the autograd thread until every rank reached that bucket)
-        if dist.is_available() and dist.is_initialized() and not _codec.is_fixed(self.params):
-            if dist.get_world_size(self.process_group) > 1:
-                self.comm_group()
+    def needs_comm_group(self) -> bool:
+        return (not _codec.is_fixed(self.params) and dist.is_available() and dist.is_initialized()
+                and dist.get_world_size(self.process_group) > 1)
 
-    def comm_group(self):
-        """The variable-rate exchange's process group: the hook's ranks, a group of its own so that its collectives
-        (issued from the comm thread) never interleave with collectives DDP issues on `process_group` from the
-        autograd thread (e.g. the find_unused_parameters all-reduce). Created with the state (or, for a state built
-        before init_process_group, by the comm thread's first exchange); only member ranks synchronise
-        (use_local_synchronization)."""
-        if self._comm_group is None:
+    def setup(self) -> "GcowHookState":
+        """Create the variable-rate exchange's process group (a collective over `process_group`'s ranks; a no-op for
+        fixed rate or a one-rank group): the hook's ranks, in a group of their own so that its collectives (issued
+        from the comm thread) never interleave with collectives DDP issues on `process_group` from the autograd
+        thread (e.g. the find_unused_parameters all-reduce). Idempotent. Returns self."""
+        if self._comm_group is None and self.needs_comm_group():
             ranks = dist.get_process_group_ranks(self.process_group or dist.group.WORLD)
             self._comm_group = dist.new_group(ranks=ranks, timeout=timedelta(seconds=self.timeout_s),
                                               use_local_synchronization=True)
+        return self
+
+    def comm_group(self):
+        """The exchange group created by setup(). Never created lazily: creating it from the comm thread would race
+        with process-group creation on the main thread, and creating it in the hook would block the autograd thread
+        until every rank reached that bucket."""
+        if self._comm_group is None:
+            raise RuntimeError("GcowHookState.setup() was not called: the variable-rate exchange needs its process "
+                               "group, created by setup() on every rank before training (or use make_hook_state)")
         return self._comm_group
 
     def _abort_comm_group(self, ex):
@@ -77,7 +89,7 @@ class GcowHookState:
         if g is None:
             return
         try:
-            g.abort()  # NCCL: tears down the communicator; peers' pending collectives error out
+            g.abort()  # NCCL/RCCL: tears down this rank's communicator (peers fail only at their timeout)
         except Exception:  # noqa: BLE001 -- gloo has no abort; destroying closes its connections
             try:
                 dist.destroy_process_group(g)
@@ -88,6 +100,11 @@ class GcowHookState:
         if dev not in self._side:
             self._side[dev] = torch.cuda.Stream(dev)
         return self._side[dev]
+
+
+def make_hook_state(**kw) -> GcowHookState:
+    """GcowHookState(**kw).setup(): call on every rank of the hook's process group at the same point of setup."""
+    return GcowHookState(**kw).setup()
 
 
 def _done(t: torch.Tensor) -> torch.futures.Future[torch.Tensor]:
@@ -142,7 +159,8 @@ class _CommWorker:
 
     Fail fast: the first exception stops the worker. That bucket's future and every future queued or submitted after
     it fail at once (DDP raises in its wait instead of hanging on a bucket that never runs), and `on_error` aborts the
-    exchange's process group so that peers blocked in a collective with this rank error out too."""
+    exchange's process group: gloo peers blocked in a collective with this rank error out at once, RCCL peers when
+    the group's timeout expires."""
 
     def __init__(self, on_error=None):
         self.q = queue.Queue()
@@ -211,6 +229,7 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
             return buf
 
         return fut.then(finish)
+    cgroup = state.comm_group() if world > 1 else group  # raises here, on the autograd thread, without setup()
     words, bits, index = cdc.encode(x, p, INDEX_STRIDE, slot=slot)
     dev = x.device
     if dev.type == "cuda":
@@ -225,7 +244,6 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
     def exchange(fut):
         if side is not None:
             torch.cuda.set_device(dev)  # this thread's current device: the bucket's, on every LOCAL_RANK
-        cgroup = state.comm_group() if world > 1 else group
         ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
         with ctx:
             if side is not None:

@@ -27,15 +27,19 @@ from ._ffi import GcowError
 
 class DeviceCodec:
     """The codec calls the exchange needs, on device tensors through libgcow.so. Encoders are cached per
-    (slot, shape, dtype, params, index stride) so a repeated bucket allocates nothing. The cache is an LRU of at most
-    `max_encoders` entries: DDP rebuilds its buckets after the first iteration (new indices and sizes), and the
-    first iteration's encoders must not hold their output / index / workspace buffers for the life of the process.
-    An evicted encoder's buffers live on while a caller still references them; callers that read them on another
-    stream record that stream on them (gcow_amd.ddp does)."""
+    (slot, shape, dtype, params, index stride) so a repeated bucket allocates nothing. Eviction is by idleness, not by
+    a fixed count: an entry not used during the last `idle_factor` x (number of cached entries) + `idle_slack` encode
+    calls is dropped. A model with B buckets reuses each key every B calls, so its steady-state encoders are never
+    evicted however large B is, while the first iteration's encoders (DDP rebuilds its buckets after it: new indices
+    and sizes) are released after a few iterations instead of holding their output / index / workspace buffers for
+    the life of the process. An evicted encoder's buffers live on while a caller still references them; callers that
+    read them on another stream record that stream on them (gcow_amd.ddp does)."""
 
-    def __init__(self, max_encoders: int = 64):
-        self._enc = OrderedDict()
-        self.max_encoders = max(1, int(max_encoders))
+    def __init__(self, idle_factor: int = 2, idle_slack: int = 8):
+        self._enc = OrderedDict()  # key -> [encoder, last tick], least recently used first
+        self.idle_factor = max(1, int(idle_factor))
+        self.idle_slack = max(0, int(idle_slack))
+        self._tick = 0
 
     def encode(self, x: torch.Tensor, params, index_stride: int = 0, slot=None):
         """-> (words int64 tensor, bits int64[1] tensor on x.device, block index or None). Calls with the same shape,
@@ -43,16 +47,25 @@ class DeviceCodec:
         another stream pass distinct slots (the DDP hook: one per bucket)."""
         from . import codec
         x = x.reshape(-1)
+        self._tick += 1
         key = (slot, x.numel(), x.dtype, x.device, params.tuple(), index_stride)
-        enc = self._enc.get(key)
-        if enc is None:
-            enc = self._enc[key] = codec.Encoder((x.numel(),), x.dtype, params, x.device, index_stride)
-            while len(self._enc) > self.max_encoders:
-                self._enc.popitem(last=False)
+        ent = self._enc.get(key)
+        if ent is None:
+            ent = self._enc[key] = [codec.Encoder((x.numel(),), x.dtype, params, x.device, index_stride), self._tick]
         else:
+            ent[1] = self._tick
             self._enc.move_to_end(key)
-        e = enc(x if x.is_contiguous() else x.contiguous())
+        self._evict_idle()
+        e = ent[0](x if x.is_contiguous() else x.contiguous())
         return e.words, e.bits_dev, e.index
+
+    def _evict_idle(self):
+        limit = self.idle_factor * len(self._enc) + self.idle_slack
+        while self._enc:
+            key, ent = next(iter(self._enc.items()))
+            if self._tick - ent[1] <= limit:
+                break
+            del self._enc[key]
 
     def stitch_shards(self, dst, src, shard_words: int, lens, nshards: int):
         from . import codec

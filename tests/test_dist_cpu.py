@@ -110,7 +110,7 @@ def _hook_worker(rank, world, port, q, hook_name, mode):
         ref.load_state_dict(model.state_dict())
         dm = nn.parallel.DistributedDataParallel(model)
         p = _params(mode)
-        dm.register_comm_hook(ddp.GcowHookState(params=p, codec=OracleCodec()), getattr(ddp, hook_name))
+        dm.register_comm_hook(ddp.make_hook_state(params=p, codec=OracleCodec()), getattr(ddp, hook_name))
         torch.manual_seed(100 + rank)  # a different batch per rank
         x = torch.randn(16, 53)
         dm(x).square().mean().backward()
@@ -171,7 +171,7 @@ def _async_hook_worker(rank, world, port, q, mode):
         from oracle_codec import OracleCodec
         p = _params(mode)
         op = O.expert(*p.tuple())
-        state = ddp.GcowHookState(params=p, codec=OracleCodec())
+        state = ddp.make_hook_state(params=p, codec=OracleCodec())
         grads = [O.gen_normal(4 * 1000 + 3, 1e-3, 300 + r, False) for r in range(world)]
         g = torch.from_numpy(grads[rank].copy())
         if rank != 0:
@@ -212,7 +212,7 @@ def _fail_fast_worker(rank, world, port, q):
                 return super().decode_mean(*a, **k)
 
         p = _params("acc1e-6")
-        state = ddp.GcowHookState(params=p, codec=Failing(), timeout_s=20.0)
+        state = ddp.make_hook_state(params=p, codec=Failing(), timeout_s=20.0)
         g = [torch.from_numpy(O.gen_normal(4 * 500 + 1, 1e-3, 40 + 10 * rank + i, False)) for i in range(2)]
         t0 = time.perf_counter()
         futs = [ddp.compressed_allgather_hook(state, _Bucket(g[i], i)) for i in range(2)]
@@ -294,7 +294,7 @@ def _ddp_register(rank, world, port, q):
         from gcow_amd import ddp
         for h in (ddp.roundtrip_hook, ddp.compressed_allgather_hook):
             m = nn.parallel.DistributedDataParallel(nn.Linear(4, 4))
-            m.register_comm_hook(ddp.GcowHookState(), h)  # DDP validates the hook signature here
+            m.register_comm_hook(ddp.make_hook_state(), h)  # DDP validates the hook signature here
         q.put((rank, True))
     except Exception as ex:
         q.put((rank, repr(ex)))
@@ -305,3 +305,72 @@ def _ddp_register(rank, world, port, q):
 def test_ddp_hooks_register():
     """gcow_amd.ddp hooks pass DDP's comm-hook signature check."""
     _run(_ddp_register, 2)
+
+
+def _state_setup_worker(rank, world, port, q):
+    _init(rank, world, port)
+    try:
+        import dataclasses
+
+        from gcow_amd import ddp
+        from oracle_codec import OracleCodec
+        p = _params("acc1e-6")
+        # construction, copies and dataclasses.replace issue no collective: rank 1 builds extra states that rank 0
+        # never builds, then both call setup() -- a mismatched new_group would hang here
+        if rank == 1:
+            for _ in range(3):
+                s = ddp.GcowHookState(params=p, codec=OracleCodec())
+                dataclasses.replace(s, timeout_s=5.0)
+        st = ddp.GcowHookState(params=p, codec=OracleCodec(), timeout_s=30.0)
+        try:
+            st.comm_group()
+            ok = False  # must refuse before setup()
+        except RuntimeError as ex:
+            ok = "setup()" in str(ex)
+        st.setup()
+        ok = ok and st.comm_group() is not None and st.setup().comm_group() is st.comm_group()  # idempotent
+        ok = ok and ddp.GcowHookState(params=_params("rate16")).setup()._comm_group is None  # fixed: no group
+        q.put((rank, True if ok else "rank %d: setup semantics" % rank))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_hook_state_setup_is_explicit():
+    """GcowHookState's constructor issues no collective (ranks may build, copy or replace states
+    independently); the variable-rate exchange group is created by setup() on every rank, and the hook refuses to
+    run without it instead of creating the group lazily on the comm thread."""
+    _run(_state_setup_worker, 2)
+
+
+def test_device_codec_cache_evicts_idle_only(monkeypatch):
+    """the DeviceCodec encoder cache keeps every key a model reuses each iteration, however many buckets
+    it has (no fixed cap that misses every step past 64 buckets), and drops the keys of buckets that stopped being
+    used (DDP's first-iteration buckets) after a few iterations. Encoder construction is stubbed (no GPU here)."""
+    from gcow_amd import codec, dist as gdist
+    built = []
+
+    class FakeEnc:
+        def __init__(self, shape, dtype, params, device, stride):
+            built.append(shape)
+
+        def __call__(self, x):
+            class E:
+                words = bits_dev = index = None
+            return E()
+
+    monkeypatch.setattr(codec, "Encoder", FakeEnc)
+    c = gdist.DeviceCodec()
+    p = codec.rate(16, 1)
+    x = torch.zeros(64)
+    first = 100  # first-iteration buckets
+    for slot in range(first):
+        c.encode(x, p, slot=("first", slot))
+    B = 300  # rebuilt buckets, more than the old fixed cap of 64
+    for it in range(6):
+        for slot in range(B):
+            c.encode(x, p, slot=slot)
+    assert len(built) == first + B  # no steady-state bucket was ever rebuilt
+    assert not any(isinstance(k[0], tuple) for k in c._enc)  # the first iteration's entries are gone
+    assert len(c._enc) == B
