@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
@@ -1920,7 +1921,7 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params
   __shared__ __attribute__((aligned(16))) uint64_t sw[vdec_cap<LANES>() + 4];
   const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
   if (vdec_left_to_big<LANES>(F, index, in_words, nchunks, base_bits, c0)) {  // workgroup-uniform
-    if (left && threadIdx.x == 0) *left = seq;  // the second pass has work (every such workgroup stores the same value)
+    if (left && threadIdx.x == 0) atomicMax((unsigned long long*)left, (unsigned long long)seq);  // second pass has work
     return;
   }
   vdec_group<LANES, vdec_cap<LANES>(), false>(F, p, in, in_words, index, nchunks, base_bits, end_out, c0, dt7, sw);
@@ -1946,7 +1947,7 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean_big(FieldDesc F, Pa
   __shared__ __attribute__((aligned(16))) uint64_t sw[vdec_cap_big<LANES>() + 4];
   __shared__ uint32_t todo[LANES];
   __shared__ uint32_t ntodo;
-  if (left && *left != seq) return;  // the main kernel left nothing (no flag buffer: check every group)
+  if (left && *left < seq) return;  // the main kernel left nothing (no flag word: check every group)
   const uint64_t ng = (nchunks + LANES - 1) / LANES;
   bool staged_tab = false;
   // sweep k: workgroup w checks groups k G LANES + t G + w (t < LANES, G = gridDim.x): the groups spread over every
@@ -2683,7 +2684,11 @@ static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, vo
         const uint32_t nc = min(CH, nfull - c0);
         const void* ic = (const char*)in + (size_t)c0 * IB;
         void* oc = (char*)out + (size_t)c0 * (WB / 8);
-        k_encode_fixed1d_np<DT, WB, 8, 256, 3><<<(nc + 2047) / 2048, 256, 0, st>>>(ic, nc, p, oc);
+#ifndef GCOW_C2_U
+#define GCOW_C2_U 8  // A/B builds only (tools/build_variant.sh -DGCOW_C2_U=4)
+#endif
+        constexpr int U = GCOW_C2_U;
+        k_encode_fixed1d_np<DT, WB, U, 256, 3><<<(nc + 256 * U - 1) / (256 * U), 256, 0, st>>>(ic, nc, p, oc);
       }
     }
   }
@@ -2807,6 +2812,35 @@ hipError_t launch_scan_blocks(const uint32_t* lens, uint32_t nblocks, uint64_t* 
   return hipGetLastError();
 }
 
+// The second-pass flag words of launch_decode1d_var: kVdecFlagRing zeroed uint64 words per device, allocated on first
+// use and kept for the life of the process (nullptr if the allocation fails: the second pass then checks every group).
+constexpr uint32_t kVdecFlagRing = 256;
+static uint64_t* vdec_flag_ring()
+{
+  static std::mutex mu;
+  static uint64_t* ring[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  if (!ring[dev]) {
+    uint64_t* r = nullptr;
+    if (hipMalloc((void**)&r, kVdecFlagRing * sizeof(uint64_t)) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    if (hipMemset(r, 0, kVdecFlagRing * sizeof(uint64_t)) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipFree(r);
+      return nullptr;
+    }
+    ring[dev] = r;
+  }
+  return ring[dev];
+}
+
 hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t in_words,
                                const uint64_t* index, uint32_t chunk, uint64_t nchunks, uint64_t base_bits,
                                uint64_t* end_out, void* stream)
@@ -2814,23 +2848,21 @@ hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64
   if (index && chunk == 16 && in_words) {  // the workgroup's stream span staged in LDS, 128 lanes
     constexpr uint32_t L = 128;
     const uint64_t ng = (nchunks + L - 1) / L;
-    // a stream-ordered flag word (its own allocation per call: decodes on other streams do not share it), set to this
-    // call's sequence number by a main-kernel workgroup that leaves its group to the second pass, so an empty second
-    // pass costs one load per workgroup instead of every group's span check (~40 us). Not initialised: a stale word
-    // equal to seq (a number no earlier call used) would only make the second pass check every group.
-    static std::atomic<uint64_t> g_seq{0x67636f77ull << 32};
-    const uint64_t seq = ++g_seq;
+    // a stream-ordered flag word: a main-kernel workgroup that leaves its group to the second pass raises the word to
+    // this call's sequence number (atomicMax), and the second pass returns at once unless the word is >= its number,
+    // so an empty second pass costs one load per workgroup instead of every group's span check (~40 us). The words
+    // are a persistent per-device ring (no allocation per call, nothing captured into a graph but the pointer):
+    // numbers only grow, so a word raised by a later call or by a concurrent decode on another stream can only make a
+    // second pass check every group (slower, still exact), never skip one that has work.
+    static std::atomic<uint64_t> g_seq{1};
+    const uint64_t seq = g_seq.fetch_add(1);
     hipStream_t st = S(stream);
-    uint64_t* left = nullptr;
-    if (hipMallocAsync((void**)&left, sizeof(uint64_t), st) != hipSuccess) {
-      (void)hipGetLastError();
-      left = nullptr;
-    }
+    uint64_t* left = vdec_flag_ring();
+    if (left) left += seq % kVdecFlagRing;
     k_decode1d_var_lean<L><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left,
                                                        seq);
     const uint32_t gbig = (uint32_t)std::min<uint64_t>(ng, 1024);
     k_decode1d_var_lean_big<L><<<gbig, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left, seq);
-    if (left) (void)hipFreeAsync(left, st);
     return hipGetLastError();
   }
   k_decode1d_var<<<(uint32_t)((nchunks + 255) / 256), 256, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, base_bits,

@@ -159,6 +159,49 @@ def test_decode_mean_bf16_output(gc, orc, mode, world, layout):
     assert bool((untouched == -1.0).all())
 
 
+@pytest.mark.parametrize("out_dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_decode_mean_stage_parts(gc, orc, world, out_dtype):
+    """k_decode_mean1d_var_lean stages each stream's span of a workgroup (128 chunks of 16 blocks) in 1, 2 or 4 parts
+    (a stage of 64 bits per block). Ranks hold data of very different magnitudes at accuracy 1e-6: N(0, 1e4) codes
+    ~137 bits per block (every group in 4 parts), N(0, 1) ~100 (2 parts), N(0, 1e-3) ~64 (1 part, or 2); inside rank 0 the
+    groups alternate between the first two. nchunks is a whole number of workgroups, so the last group's span runs to
+    stream_words, far past the shorter ranks' streams. Bit-exact vs the oracle mean, fp32 and bf16 out."""
+    wg = 128 * 16 * 4  # values per workgroup
+    n = wg * 7
+    rng = np.random.default_rng(31337 + world)
+    scales = [1e4, 1.0, 1e-3]
+    buckets = []
+    for r in range(world):
+        a = rng.standard_normal(n).astype(np.float32) * np.float32(scales[r])
+        if r == 0:
+            for g in range(1, 7, 2):
+                a[g * wg:(g + 1) * wg] *= np.float32(1e-4)  # groups at ~N(0, 1): 2 parts
+        buckets.append(a)
+    op = orc.accuracy(1e-6)
+    p = _P(gc, op)
+    encs = [gc.encode(_dev(b), p, index_stride=16) for b in buckets]
+    lens = [e.bits for e in encs]
+    bpb = [b / (n // 4) for b in lens]
+    assert bpb[0] > 100 and (world < 2 or 80 < bpb[1] < 128) and (world < 3 or bpb[2] < 72), bpb
+    sw = max((b + 63) // 64 for b in lens) + 1
+    streams = torch.zeros(world * sw + 2, dtype=torch.int64, device="cuda")
+    for r, e in enumerate(encs):
+        streams[r * sw:r * sw + e.nwords] = e.stream()
+    ni = encs[0].index.numel()
+    idx = torch.cat([e.index[:ni] for e in encs])
+    want = _oracle_mean(orc, [orc.compress(b, op)[0] for b in buckets], op, n)
+    if out_dtype == "f32":
+        got = gc.decode_mean(streams, sw, world, n, p, idx, ni, 16)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    else:
+        out = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+        gc.decode_mean(streams, sw, world, n, p, idx, ni, 16, out=out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().view(torch.int16).numpy().view(np.uint16), _bf16_rne(want))
+
+
 @pytest.mark.parametrize("mode", ["rate16", "acc1e-6"])
 def test_decode_mean_full_size_w8(gc, orc, mode):
     """The hook's receive side at the bench's size: 8 streams of 256 Mi fp32 values (8 different buckets, the bench's
@@ -286,7 +329,7 @@ def _mp_worker(rank, world, port, q, what, mode):
             refm = nn.Linear(67, 61, bias=False)
             refm.load_state_dict(model.state_dict())
             dm = nn.parallel.DistributedDataParallel(model)
-            dm.register_comm_hook(ddp.GcowHookState(params=p, codec=cdc), ddp.compressed_allgather_hook)
+            dm.register_comm_hook(ddp.make_hook_state(params=p, codec=cdc), ddp.compressed_allgather_hook)
             torch.manual_seed(10 + rank)
             x = torch.randn(8, 67)
             dm(x).square().mean().backward()
@@ -360,7 +403,7 @@ def test_ddp_hooks_world1_bit_exact(gc, orc, nccl_world1, hook, mode):
         seen.append(bucket.index())
         return getattr(ddp, hook)(state, bucket)
 
-    dm.register_comm_hook(ddp.GcowHookState(params=params), counted)
+    dm.register_comm_hook(ddp.make_hook_state(params=params), counted)
     op = orc.expert(*params.tuple())
     for step in range(2):
         model.zero_grad()
@@ -391,7 +434,7 @@ def test_ddp_allgather_hook_bf16_world1(gc, orc, nccl_world1, mode, hook):
     model, ref = layers(), layers()
     ref.load_state_dict(model.state_dict())
     dm = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=1)
-    dm.register_comm_hook(ddp.GcowHookState(params=params), getattr(ddp, hook))
+    dm.register_comm_hook(ddp.make_hook_state(params=params), getattr(ddp, hook))
     op = orc.expert(*params.tuple())
     for step in range(2):
         model.zero_grad()
@@ -426,7 +469,7 @@ def test_allgather_hook_delayed_decode_stream(gc, orc, nccl_world1):
     model, ref = layers(), layers()
     ref.load_state_dict(model.state_dict())
     dm = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=1)
-    dm.register_comm_hook(ddp.GcowHookState(params=params, codec=Delayed()), ddp.compressed_allgather_hook)
+    dm.register_comm_hook(ddp.make_hook_state(params=params, codec=Delayed()), ddp.compressed_allgather_hook)
     op = orc.expert(*params.tuple())
     for step in range(2):
         model.zero_grad()
