@@ -18,7 +18,8 @@ Extra objects on the same JSON line (they never change `value`):
   N > 1:  encode_allgather (C4 exchange: encode + RCCL all-gather of the compressed shards, gathered stream checked
           against the oracle on sampled ranges of every shard), subgroups (1/2/4/.. ranks over dist.new_group),
           strong (8 GiB split k ways), c5_sharded (bf16 accuracy 1e-6: encode + length exchange + padded all-gather
-          + one-launch stitch, checked against the oracle at every shard start)
+          + one-launch stitch, checked against the oracle at every shard start), hook_exchange (the DDP hook's whole
+          exchange: all-gather + decode-mean of every stream vs the sharded receive, both checked)
   N = 1:  host_e2e (pinned H2D + encode + D2H; PCIe-inclusive), configs (C2 rate 8 encode and rate 16 decode, C3 512^3
           rate 8 / accuracy 1e-3 encode + decode, C5 bf16 accuracy 1e-6 / 1e-3 device and host path), cpu_baseline
 Prints ONE JSON line on rank 0.
@@ -374,6 +375,81 @@ def leg_c5_sharded(ctx, n):
             "stitched_stream_matches_oracle": ok}
 
 
+def leg_hook_exchange(ctx, n):
+    """The DDP hook's whole exchange at N ranks on one 256 Mi-value fp32 bucket per rank (rate 16 and accuracy 1e-6,
+    the caller's defaults): `allgather` = encode, all-gather of the streams (lengths first for variable rate), one
+    decode-mean of all W streams (ddp.compressed_allgather_hook); `sharded` = encode, cut positions, all-to-all of
+    the shard pieces, one decode-mean of this rank's shard, all-gather of the mean shards
+    (ddp.compressed_sharded_hook). Both give the same bucket bit for bit (checked); rank 0 also checks the first
+    64 Ki values of the sharded result against the oracle's mean of every rank's decode."""
+    import numpy as np
+
+    from gcow_amd import codec
+    from gcow_amd import dist as gdist
+    W = ctx.world
+    x = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+    codec.fill_normal(x, 1e-3, seed=SEED + 77 + ctx.rank, inject=True)
+    out = {}
+    for name, p, stride in (("rate16", codec.rate(16, 1), 0), ("acc1e-6", codec.accuracy(1e-6), 16)):
+        enc = codec.Encoder((n,), torch.float32, p, ctx.dev, index_stride=stride)
+        ag = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+        sh = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+
+        def allgather_path():
+            e = enc(x)
+            if stride:
+                _, lens_h = gdist.gather_lengths(e.bits_dev, ctx.dev)
+                sw = max(1, max((b + 63) // 64 for b in lens_h))
+                g = gdist.allgather_padded(e.words, (lens_h[ctx.rank] + 63) // 64, sw, pad=2)
+                ni = e.index.numel()
+                idx = torch.empty(W * ni, dtype=torch.int64, device=ctx.dev)
+                gdist.allgather_into(idx, e.index[:ni].contiguous())
+                codec.decode_mean(g, sw, W, n, p, idx, ni, stride, out=ag)
+            else:
+                nw = ((n + 3) // 4 * p.maxbits + 63) // 64
+                g = torch.zeros(W * nw + 2, dtype=torch.int64, device=ctx.dev)
+                gdist.allgather_into(g[: W * nw], e.words[:nw].contiguous())
+                codec.decode_mean(g, nw, W, n, p, out=ag)
+
+        def sharded_path():
+            e = enc(x)
+            if stride:
+                pieces, pw, pidx, iw, lo, hi = gdist.shard_pieces_variable(e.words, e.bits_dev, e.index, n, stride)
+            else:
+                pieces, pw, lo, hi = gdist.shard_pieces_fixed(e.words, n, p.maxbits)
+                pidx, iw = None, 0
+            shard = sh[lo:hi]
+            if hi > lo:
+                codec.decode_mean(pieces, pw, W, hi - lo, p, pidx, iw, stride, out=shard)
+            gdist.allgather_shards(sh, shard, n)
+
+        a_ms, _ = timed(ctx, allgather_path, 1, 4)
+        s_ms, _ = timed(ctx, sharded_path, 1, 4)
+        a_ms, s_ms = ctx.max_over_ranks([a_ms, s_ms])
+        same = bool(torch.equal(ag.view(torch.int32), sh.view(torch.int32)))
+        same = bool(ctx.max_over_ranks([0.0 if same else 1.0])[0] == 0.0)
+        ok = None
+        if ctx.rank == 0:
+            from oracle import oracle as O
+            op = O.expert(*p.tuple())
+            m = 1 << 16
+            y = torch.empty(n, dtype=torch.float32, device=ctx.dev)
+            acc = np.zeros(m, np.float32)
+            for r in range(W):
+                codec.fill_normal(y, 1e-3, seed=SEED + 77 + r, inject=True)
+                a = y[:m].cpu().numpy()
+                acc = acc + O.decompress(O.compress(a, op)[0], (m,), op)
+            want = acc / np.float32(W)
+            ok = bool(np.array_equal(sh[:m].cpu().numpy().view(np.uint32), want.view(np.uint32))) and same
+            del y
+        out[name] = {"allgather_exchange_ms": round(a_ms, 4), "sharded_exchange_ms": round(s_ms, 4),
+                     "sharded_equals_allgather": same, "sharded_mean_matches_oracle": ok}
+        del enc, ag, sh
+        torch.cuda.empty_cache()
+    del x
+    return out
+
+
 def leg_host_e2e(ctx, enc, x, p, n, in_bytes, out_bytes):
     from gcow_amd import codec
     h_in = x.cpu().pin_memory()
@@ -571,12 +647,52 @@ def leg_decode_mean(ctx, W: int = 8):
                        stream=st)
         k = sum(per) / len(per)
         kname = "k_decode_mean_fixed1d<64>" if stride == 0 else "k_decode_mean1d_var<128>"
+        # the sharded receive (ddp.compressed_sharded_hook): one rank's decode-mean of its 1/W shard from the W pieces
+        # the all-to-all delivers (cut here from the same streams; the exchange itself is an N > 1 leg)
+        pieces, pw, pidx, iw, lo, hi = shard0_pieces(buf, sw, W, n, p, ix, ni)
+        shard = mean[lo:hi]
+        _, sper = timed(ctx, lambda: codec.decode_mean(pieces, pw, W, hi - lo, p, pidx, iw, stride, out=shard,
+                                                       stream=st), 3, 10, stream=st)
+        ks = sum(sper) / len(sper)
         res[name] = {"streams": W, "values": n, "kernel_ms": round(k, 4), "bits_per_value": round(bits / W / n, 3),
-                     "roofline": roof(bits / 8, n * 4, k, kname, basis="write")}
-        del buf, ix
+                     "roofline": roof(bits / 8, n * 4, k, kname, basis="write"),
+                     "sharded_receive_kernel_ms": round(ks, 4), "sharded_receive_values": hi - lo}
+        del buf, ix, pieces, pidx
         torch.cuda.empty_cache()
     del x, mean
     return res
+
+
+def shard0_pieces(buf, sw, W, n, p, ix, ni, index_stride=16):
+    """What rank 0 of a W-rank ddp.compressed_sharded_hook holds after its all-to-all, built locally from W streams
+    laid out sw words apart (with their block indexes, ni entries apart, for variable rate): every stream cut at rank
+    0's shard (gcow_amd.dist.shard_plan) -- fixed rate at b * maxbits, variable rate at the index, the index slice
+    rebased to the piece's first word. -> (pieces, piece_words, index or None, index_words, lo, hi)."""
+    from gcow_amd import codec
+    from gcow_amd import dist as gdist
+    bounds, per = gdist.shard_plan(n, W)
+    lo, hi = bounds[0]
+    nb = (n + 3) // 4
+    b1 = min((hi + 3) // 4, nb)
+    dev = buf.device
+    if codec.is_fixed(p):
+        pw = (b1 * p.maxbits + 63) // 64
+        pieces = torch.zeros(W * pw + 2, dtype=torch.int64, device=dev)
+        for s in range(W):
+            pieces[s * pw:(s + 1) * pw] = buf[s * sw:s * sw + pw]
+        return pieces, pw, None, 0, lo, hi
+    nc = (b1 + index_stride - 1) // index_stride
+    ends = ix.view(W, ni)[:, nc].tolist() if nc < ni else None
+    pw = 1
+    for s in range(W):
+        end_bit = ends[s] if ends is not None else 64 * sw
+        pw = max(pw, (end_bit + 63) // 64)
+    pieces = torch.zeros(W * pw + 2, dtype=torch.int64, device=dev)
+    pidx = torch.empty(W * nc, dtype=torch.int64, device=dev)
+    for s in range(W):  # rank 0's shard starts at bit 0 of every stream
+        pieces[s * pw:(s + 1) * pw] = buf[s * sw:s * sw + pw]
+        pidx[s * nc:(s + 1) * nc] = ix[s * ni:s * ni + nc]
+    return pieces, pw, pidx, nc, lo, hi
 
 
 def _cpu_model() -> str:
@@ -807,6 +923,8 @@ def worker(args):
             torch.cuda.empty_cache()
             extra["strong"] = leg_strong(ctx, p, int(args.strong_gib * (1 << 30)) // 4)
             extra["c5_sharded"] = leg_c5_sharded(ctx, args.c5_values)
+            torch.cuda.empty_cache()
+            extra["hook_exchange"] = leg_hook_exchange(ctx, args.c5_values)
         else:
             extra["host_e2e"] = leg_host_e2e(ctx, lambda t: enc(t, stream), x, p, n, in_bytes, out_bytes)
             extra["configs"] = leg_configs(ctx)

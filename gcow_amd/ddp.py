@@ -61,12 +61,13 @@ class GcowHookState:
         return self._worker
 
     def needs_comm_group(self) -> bool:
-        return (not _codec.is_fixed(self.params) and dist.is_available() and dist.is_initialized()
-                and dist.get_world_size(self.process_group) > 1)
+        """An exchange group exists for every multi-rank state: the variable-rate all-gather hook and the sharded
+        hook (any rate) run their collectives on the comm thread over it."""
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.process_group) > 1
 
     def setup(self) -> "GcowHookState":
-        """Create the variable-rate exchange's process group (a collective over `process_group`'s ranks; a no-op for
-        fixed rate or a one-rank group): the hook's ranks, in a group of their own so that its collectives (issued
+        """Create the exchange's process group (a collective over `process_group`'s ranks; a no-op for a one-rank
+        group): the hook's ranks, in a group of their own so that its collectives (issued
         from the comm thread) never interleave with collectives DDP issues on `process_group` from the autograd
         thread (e.g. the find_unused_parameters all-reduce). Idempotent. Returns self."""
         if self._comm_group is None and self.needs_comm_group():
@@ -260,6 +261,64 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
             _mean_into(cdc, flat, gathered, maxw, world, n, p, idx, ni, INDEX_STRIDE)
             # completed inside the side-stream context: the future records its event on this stream, so DDP's wait
             # orders its use of the bucket after the mean is written
+            fut.set_result(buf)
+
+    return state.worker().submit(exchange, fut)
+
+
+def compressed_sharded_hook(state: GcowHookState, bucket) -> torch.futures.Future[torch.Tensor]:
+    """The compressed exchange with a sharded receive side (gcow_amd.dist "sharded receive"): each rank encodes its
+    bucket, cuts its stream at the shard boundaries (fixed rate: at b * maxbits; variable rate: at the block index)
+    and sends piece r to rank r in one all-to-all; rank r decodes and averages the W pieces of its shard in one launch
+    (gcow_decode_mean_device), and an all-gather of the mean shards (in the bucket's dtype: fp32, or bf16 rounded to
+    nearest even in the kernel) rebuilds the bucket on every rank. The result is bit-identical to
+    compressed_allgather_hook's (the same fp32 sums in rank order); per rank it receives (W - 1) / W of one stream
+    instead of W - 1 streams and decodes 1 / W of the values, for an extra all-gather of the mean. Collectives run on
+    the state's comm thread over its exchange group (GcowHookState.setup, every rank), on a side stream that waits
+    for the encode; the returned future completes when the bucket holds the mean."""
+    group = state.process_group
+    buf = bucket.buffer()
+    world = dist.get_world_size(group)
+    flat, x = _flat(buf)
+    n = x.numel()
+    p = state.params
+    cdc = state.get_codec()
+    fixed = _codec.is_fixed(p)
+    stride = 0 if fixed else INDEX_STRIDE
+    cgroup = state.comm_group() if world > 1 else group  # raises here, on the autograd thread, without setup()
+    slot = ("sharded", bucket.index() if hasattr(bucket, "index") else None)
+    words, bits, index = cdc.encode(x, p, stride, slot=slot)
+    dev = x.device
+    if dev.type == "cuda":
+        ev = torch.cuda.Event()
+        ev.record()
+        side = state.side_stream(dev)
+        fut = torch.futures.Future(devices=[dev])
+    else:
+        ev = side = None
+        fut = torch.futures.Future()
+
+    def exchange(fut):
+        if side is not None:
+            torch.cuda.set_device(dev)
+        ctx = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
+        with ctx:
+            if side is not None:
+                side.wait_event(ev)
+                for t in (words, bits, index):
+                    if t is not None:
+                        t.record_stream(side)
+            if fixed:
+                pieces, pw, lo, hi = gdist.shard_pieces_fixed(words, n, p.maxbits, cgroup)
+                pidx, iw = None, 0
+            else:
+                pieces, pw, pidx, iw, lo, hi = gdist.shard_pieces_variable(words, bits, index, n, INDEX_STRIDE,
+                                                                            cgroup)
+            direct = flat.dtype in (torch.float32, torch.bfloat16) and flat.is_contiguous()
+            shard = flat[lo:hi] if direct else torch.empty(hi - lo, dtype=torch.float32, device=dev)
+            if hi > lo:
+                cdc.decode_mean(pieces, pw, world, hi - lo, p, pidx, iw, stride, out=shard)
+            gdist.allgather_shards(flat, shard if direct else shard.to(flat.dtype), n, cgroup)
             fut.set_result(buf)
 
     return state.worker().submit(exchange, fut)

@@ -197,3 +197,116 @@ def encode_allgather(bucket: torch.Tensor, params, group=None, codec=None):
     if fixed:  # ragged shards: the bit counts are known on the host
         bits = nb * params.maxbits
     return allgather_variable(words, bits, group, codec)
+
+
+# ---------------------------------------------------------------------------------------------- sharded receive
+# The receive side of the compressed DDP exchange without decoding every rank's whole stream on every rank: rank r
+# owns one block-aligned shard of the bucket. Every rank cuts its own stream at the shard boundaries (fixed rate: at
+# b * maxbits; variable rate: at the block index), sends piece r to rank r (one all-to-all), rank r decodes and
+# averages the W pieces of its shard (gcow_decode_mean_device on W "streams" of one shard -- the same per-value
+# arithmetic, in the same rank order, as decoding the whole streams), and one all-gather of the mean shards rebuilds
+# the bucket on every rank. Per rank, against all-gathering the streams and decoding them all: (W - 1) / W of ONE
+# stream received instead of W - 1 streams, 1 / W of the decode work, plus the all-gather of the mean (fp32 / bf16).
+SHARD_ALIGN_BLOCKS = 64  # shard starts on 64-block multiples: a whole 16-block index chunk, and 64 maxbits % 64 == 0
+
+
+def shard_plan(nvals: int, world: int):
+    """Block-aligned shards [lo, hi) (values) of a 1-D bucket for every rank, and the values in a full shard."""
+    bounds = [shard_bounds(nvals, world, r, align_blocks=SHARD_ALIGN_BLOCKS) for r in range(world)]
+    per = max(hi - lo for lo, hi in bounds)
+    return bounds, per
+
+
+def alltoall_into(out: torch.Tensor, inp: torch.Tensor, group=None):
+    """Equal-split all-to-all: chunk r of `inp` to rank r, chunk s of `out` from rank s."""
+    dist.all_to_all_single(out, inp, group=group)
+    return out
+
+
+def shard_pieces_fixed(words: torch.Tensor, nvals: int, maxbits: int, group=None):
+    """Fixed rate: this rank's stream cut at the shard boundaries and exchanged. Returns (pieces, piece_words, lo,
+    hi): pieces holds rank s's piece of this rank's shard at s * piece_words (+ 2 zero words), [lo, hi) the shard."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    bounds, per = shard_plan(nvals, world)
+    pw = max(1, (per // 4) * maxbits // 64)
+    nb = (nvals + 3) // 4
+    send = torch.zeros(world * pw, dtype=torch.int64, device=words.device)
+    for r, (lo, hi) in enumerate(bounds):
+        w0 = (lo // 4) * maxbits // 64
+        w1 = (min((hi + 3) // 4, nb) * maxbits + 63) // 64
+        if w1 > w0:
+            send[r * pw:r * pw + (w1 - w0)] = words[w0:w1]
+    pieces = torch.zeros(world * pw + 2, dtype=torch.int64, device=words.device)
+    alltoall_into(pieces[: world * pw], send, group)
+    lo, hi = bounds[rank]
+    return pieces, pw, lo, hi
+
+
+def shard_pieces_variable(words: torch.Tensor, bits, index: torch.Tensor, nvals: int, index_stride: int = 16,
+                          group=None):
+    """Variable rate (block index every `index_stride` blocks): this rank's stream cut at the shard boundaries (the
+    bit where each shard's first block starts, from the index), every piece starting at the stream word that holds
+    its first bit, and its index entries rebased to that word. One all-gather of every rank's W + 1 cut positions
+    (the host read that sizes the padded pieces), then two all-to-alls (words, index). Returns (pieces, piece_words,
+    pidx, pidx_words, lo, hi): rank s's piece of this rank's shard at s * piece_words (+ 2 zero words) with its index
+    at s * pidx_words."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    bounds, per = shard_plan(nvals, world)
+    dev = words.device
+    nb = (nvals + 3) // 4
+    assert SHARD_ALIGN_BLOCKS % index_stride == 0
+    starts = [lo // 4 // index_stride for lo, _ in bounds]  # index chunk of each shard's first block
+    bits_t = bits.reshape(1).to(device=dev, dtype=torch.int64) if isinstance(bits, torch.Tensor) else \
+        torch.tensor([int(bits)], dtype=torch.int64, device=dev)
+    cut = torch.empty(world + 1, dtype=torch.int64, device=dev)
+    for r, (lo, hi) in enumerate(bounds):  # an empty shard (lo = nvals) starts at the stream's end
+        if lo // 4 < nb:
+            cut[r:r + 1] = index[starts[r]:starts[r] + 1]
+        else:
+            cut[r:r + 1] = bits_t
+    cut[world:] = bits_t
+    allcuts = torch.empty(world * (world + 1), dtype=torch.int64, device=dev)
+    allgather_into(allcuts, cut, group)
+    C_h = [int(v) for v in allcuts.tolist()]  # the one host read: sizes the padded pieces
+    def span(c0, c1):
+        return (c0 >> 6, (c1 + 63) >> 6 if c1 > c0 else c0 >> 6)
+    pw = 1
+    for s in range(world):
+        cs = C_h[s * (world + 1):(s + 1) * (world + 1)]
+        for r in range(world):
+            a, b = span(cs[r], cs[r + 1])
+            pw = max(pw, b - a)
+    mine = C_h[rank * (world + 1):(rank + 1) * (world + 1)]
+    nchunk = [(min((hi + 3) // 4, nb) - lo // 4 + index_stride - 1) // index_stride if hi > lo else 0
+              for lo, hi in bounds]
+    iw = max(1, max(nchunk))
+    send = torch.zeros(world * pw, dtype=torch.int64, device=dev)
+    isend = torch.zeros(world * iw, dtype=torch.int64, device=dev)
+    for r in range(world):
+        a, b = span(mine[r], mine[r + 1])
+        if b > a:
+            send[r * pw:r * pw + (b - a)] = words[a:b]
+        if nchunk[r]:
+            isend[r * iw:r * iw + nchunk[r]] = index[starts[r]:starts[r] + nchunk[r]] - 64 * a
+    pieces = torch.zeros(world * pw + 2, dtype=torch.int64, device=dev)
+    alltoall_into(pieces[: world * pw], send, group)
+    pidx = torch.empty(world * iw, dtype=torch.int64, device=dev)
+    alltoall_into(pidx, isend, group)
+    lo, hi = bounds[rank]
+    return pieces, pw, pidx, iw, lo, hi
+
+
+def allgather_shards(flat: torch.Tensor, shard: torch.Tensor, nvals: int, group=None):
+    """Every rank's decoded shard (shard_plan bounds; `shard` = this rank's values) gathered into `flat` (n values,
+    the bucket, any dtype)."""
+    world = dist.get_world_size(group)
+    _, per = shard_plan(nvals, world)
+    mine = torch.zeros(per, dtype=flat.dtype, device=flat.device)
+    mine[: shard.numel()] = shard
+    if flat.is_contiguous() and flat.numel() == world * per:
+        allgather_into(flat, mine, group)  # straight into the bucket
+    else:
+        full = torch.empty(world * per, dtype=flat.dtype, device=flat.device)
+        allgather_into(full, mine, group)
+        flat.copy_(full[: flat.numel()])
+    return flat

@@ -119,7 +119,7 @@ def _hook_worker(rank, world, port, q, hook_name, mode):
         allg = [torch.empty_like(local) for _ in range(world)]
         dist.all_gather(allg, local)
         op = O.expert(*p.tuple())
-        if hook_name == "compressed_allgather_hook":
+        if hook_name in ("compressed_allgather_hook", "compressed_sharded_hook"):
             acc = np.zeros(local.numel(), np.float32)
             for g in allg:
                 w, _ = O.compress(g.numpy(), op)
@@ -138,6 +138,15 @@ def _hook_worker(rank, world, port, q, hook_name, mode):
         q.put((rank, repr(ex)))
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("mode", ["rate16", "acc1e-6", "rate2.5"])
+def test_compressed_sharded_hook_gloo(world, mode):
+    """The sharded-receive hook end to end over gloo (cut positions all-gather, word and index all-to-alls, one
+    decode-mean of the rank's shard, all-gather of the mean shards): bit-identical to the all-gather hook's result,
+    the oracle's mean of decode(encode(each rank's gradient))."""
+    _run(_hook_worker, world, "compressed_sharded_hook", mode)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -329,7 +338,7 @@ def _state_setup_worker(rank, world, port, q):
             ok = "setup()" in str(ex)
         st.setup()
         ok = ok and st.comm_group() is not None and st.setup().comm_group() is st.comm_group()  # idempotent
-        ok = ok and ddp.GcowHookState(params=_params("rate16")).setup()._comm_group is None  # fixed: no group
+        ok = ok and ddp.GcowHookState(params=_params("rate16")).setup()._comm_group is not None  # any rate
         q.put((rank, True if ok else "rank %d: setup semantics" % rank))
     except Exception as ex:  # pragma: no cover
         q.put((rank, repr(ex)))
@@ -374,3 +383,57 @@ def test_device_codec_cache_evicts_idle_only(monkeypatch):
     assert len(built) == first + B  # no steady-state bucket was ever rebuilt
     assert not any(isinstance(k[0], tuple) for k in c._enc)  # the first iteration's entries are gone
     assert len(c._enc) == B
+
+
+def _sharded_exchange_worker(rank, world, port, q, mode, nvals, bf16):
+    _init(rank, world, port)
+    try:
+        from gcow_amd import codec
+        from gcow_amd import dist as gdist
+        from oracle import oracle as O
+        from oracle_codec import OracleCodec
+        p = _params(mode)
+        op = O.expert(*p.tuple())
+        cdc = OracleCodec()
+        grads = []
+        for r in range(world):
+            a = O.gen_normal(nvals, 1e-3, 500 + r, True)
+            if bf16:
+                a = (a.view(np.uint32) >> 16).astype(np.uint16)
+            grads.append(a)
+        mine = torch.from_numpy(grads[rank].copy())
+        x = mine.view(torch.bfloat16) if bf16 else mine
+        fixed = codec.is_fixed(p)
+        words, bits, index = cdc.encode(x, p, 0 if fixed else 16)
+        if fixed:
+            pieces, pw, lo, hi = gdist.shard_pieces_fixed(words, nvals, p.maxbits)
+            pidx, iw = None, 0
+        else:
+            pieces, pw, pidx, iw, lo, hi = gdist.shard_pieces_variable(words, bits, index, nvals, 16)
+        flat = torch.full((nvals,), -7.0, dtype=torch.float32)
+        shard = flat[lo:hi]
+        if hi > lo:
+            cdc.decode_mean(pieces, pw, world, hi - lo, p, pidx, iw, 0 if fixed else 16, out=shard)
+        gdist.allgather_shards(flat, shard, nvals)
+        acc = np.zeros(nvals, np.float32)
+        for a in grads:
+            acc = acc + O.decompress(O.compress(a, op)[0], (nvals,), op)
+        want = acc / np.float32(world)
+        ok = np.array_equal(flat.numpy().view(np.uint32), want.view(np.uint32))
+        q.put((rank, True if ok else "rank %d: mean over shards != oracle mean (shard %d..%d)" % (rank, lo, hi)))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("mode,nvals,bf16", [("rate16", 4 * 3000 + 2, False), ("rate2.5", 4 * 3001 + 1, False),
+                                             ("acc1e-6", 4 * 3000 + 3, False), ("acc1e-3", 4 * 2999, True),
+                                             ("acc1e-6", 300, False), ("rate16", 300, False)])
+def test_sharded_pieces_gloo(world, mode, nvals, bf16):
+    """gcow_amd.dist's sharded receive on its own (the exchange under compressed_sharded_hook): streams cut at 64-block
+    shard boundaries, pieces and rebased index slices all-to-all'd, the shard's mean decoded from W pieces, the mean
+    shards all-gathered -- equal, bit for bit, to the mean of the oracle decodes of the whole streams. Ragged last
+    shards, partial last blocks, bf16 buckets, and buckets too small for every rank to own a shard (empty shards)."""
+    _run(_sharded_exchange_worker, world, mode, nvals, bf16)

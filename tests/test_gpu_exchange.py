@@ -329,7 +329,8 @@ def _mp_worker(rank, world, port, q, what, mode):
             refm = nn.Linear(67, 61, bias=False)
             refm.load_state_dict(model.state_dict())
             dm = nn.parallel.DistributedDataParallel(model)
-            dm.register_comm_hook(ddp.make_hook_state(params=p, codec=cdc), ddp.compressed_allgather_hook)
+            hook = ddp.compressed_sharded_hook if what == "sharded_hook" else ddp.compressed_allgather_hook
+            dm.register_comm_hook(ddp.make_hook_state(params=p, codec=cdc), hook)
             torch.manual_seed(10 + rank)
             x = torch.randn(8, 67)
             dm(x).square().mean().backward()
@@ -351,7 +352,8 @@ def _mp_worker(rank, world, port, q, what, mode):
 
 
 @pytest.mark.parametrize("what,mode", [("encode_allgather", "rate16"), ("encode_allgather", "acc1e-6"),
-                                       ("encode_allgather", "bf16_acc1e-3"), ("hook", "rate16"), ("hook", "acc1e-6")])
+                                       ("encode_allgather", "bf16_acc1e-3"), ("hook", "rate16"), ("hook", "acc1e-6"),
+                                       ("sharded_hook", "rate16"), ("sharded_hook", "acc1e-6")])
 @pytest.mark.parametrize("world", [2, 3])
 def test_exchange_multiprocess_device_codec(gc, what, mode, world):
     import torch.multiprocessing as mp
@@ -381,7 +383,7 @@ def nccl_world1():
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("hook", ["roundtrip_hook", "compressed_allgather_hook"])
+@pytest.mark.parametrize("hook", ["roundtrip_hook", "compressed_allgather_hook", "compressed_sharded_hook"])
 @pytest.mark.parametrize("mode", ["rate16", "acc1e-6", "rate8", "expert_var_minbits", "expert_var_trunc"])
 def test_ddp_hooks_world1_bit_exact(gc, orc, nccl_world1, hook, mode):
     """One rank over RCCL: every weight gradient equals the oracle's decode(encode(local grad)) -- (0 + x) / 1 for the
@@ -414,13 +416,13 @@ def test_ddp_hooks_world1_bit_exact(gc, orc, nccl_world1, hook, mode):
         for lm, lr in zip(model, ref):
             g = lr.weight.grad.reshape(-1).cpu().numpy()
             dec = orc.decompress(orc.compress(g, op)[0], g.shape, op)
-            want = (np.zeros_like(dec) + dec) / np.float32(1) if hook == "compressed_allgather_hook" else dec
+            want = (np.zeros_like(dec) + dec) / np.float32(1) if hook != "roundtrip_hook" else dec
             got = lm.weight.grad.reshape(-1).cpu().numpy()
             assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), step
     assert len(set(seen)) >= 2, seen  # several buckets per step
 
 
-@pytest.mark.parametrize("hook", ["roundtrip_hook", "compressed_allgather_hook"])
+@pytest.mark.parametrize("hook", ["roundtrip_hook", "compressed_allgather_hook", "compressed_sharded_hook"])
 @pytest.mark.parametrize("mode", ["rate16", "acc1e-6"])
 def test_ddp_allgather_hook_bf16_world1(gc, orc, nccl_world1, mode, hook):
     """bf16 model over RCCL: both hooks decode straight into the bf16 bucket; every weight gradient equals the
@@ -445,7 +447,7 @@ def test_ddp_allgather_hook_bf16_world1(gc, orc, nccl_world1, mode, hook):
         for lm, lr in zip(model, ref):
             gb = lr.weight.grad.reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
             dec = orc.decompress(orc.compress(gb, op)[0], gb.shape, op)
-            want = _bf16_rne((np.zeros_like(dec) + dec) / np.float32(1) if hook == "compressed_allgather_hook" else dec)
+            want = _bf16_rne((np.zeros_like(dec) + dec) / np.float32(1) if hook != "roundtrip_hook" else dec)
             got = lm.weight.grad.reshape(-1).view(torch.int16).cpu().numpy().view(np.uint16)
             assert np.array_equal(got, want), step
 
@@ -487,7 +489,8 @@ def test_allgather_hook_delayed_decode_stream(gc, orc, nccl_world1):
 # ---------------------------------------------------------------------------------------------- bench N > 1 legs
 def test_bench_multi_legs_world1(gc):
     """bench.py's multi-GPU legs (C4 exchange with the oracle check of the gathered stream, the sub-communicator
-    curve, strong scaling, C5 sharded with the stitch checked against the oracle) run on the GPU over a one-rank RCCL
+    curve, strong scaling, C5 sharded with the stitch checked against the oracle, the hook exchange in both forms)
+    run on the GPU over a one-rank RCCL
     group (--multi-legs), small sizes: the code the driver's 8-GPU run executes, exercised on a one-GPU box."""
     import json
     import subprocess
@@ -507,3 +510,6 @@ def test_bench_multi_legs_world1(gc):
     assert d["encode_allgather"]["gathered_stream_matches_oracle"] is True
     assert d["c5_sharded"]["stitched_stream_matches_oracle"] is True
     assert [c["k"] for c in d["subgroups"]] == [1] and [c["k"] for c in d["strong"]["curve"]] == [1]
+    for mode in ("rate16", "acc1e-6"):  # the DDP hook's exchange: all-gather form vs sharded receive
+        h = d["hook_exchange"][mode]
+        assert h["sharded_equals_allgather"] is True and h["sharded_mean_matches_oracle"] is True, h
