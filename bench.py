@@ -156,6 +156,18 @@ def timed(ctx: Ctx, step, warmup: int, steps: int, group=None, stream=None):
     return wall, per
 
 
+def steady_ms(ctx: Ctx, step, stream, settle_s: float = 0.25, steps: int = 50) -> float:
+    """The same step's HIP-event time once the clock has settled under load (settle_s of back-to-back steps first):
+    the sustained figure beside the driver-protocol one (5 + 20 launches, inside the DVFS dip)."""
+    t_end = time.perf_counter() + settle_s
+    while time.perf_counter() < t_end:
+        for _ in range(10):
+            step()
+        ctx.sync()
+    _, per = timed(ctx, step, 0, steps, stream=stream)
+    return round(sum(per) / len(per), 4)
+
+
 def gib(nbytes: float, ms: float) -> float:
     return nbytes / (ms / 1e3) / 2 ** 30
 
@@ -507,6 +519,7 @@ def leg_configs(ctx):
     w8, per = timed(ctx, lambda: enc8(x, st), 5, 20, stream=st)
     k8 = sum(per) / len(per)
     out["c2_rate8"] = {"ms_per_step": round(w8, 4), "GiBps_input": round(gib(n * 4, w8), 2), "kernel_ms": round(k8, 4),
+                       "steady_ms": steady_ms(ctx, lambda: enc8(x, st), st),
                        "encode_roofline": roof(n * 4, n, k8, "k_encode_fixed1d_np<F32, 32>")}
     del enc8
     enc16 = codec.Encoder((n,), torch.float32, codec.rate(16, 1), ctx.dev)
@@ -516,6 +529,7 @@ def leg_configs(ctx):
     dk = sum(dper) / len(dper)
     out["c2_rate16_decode"] = {"ms_per_step": round(wd, 4), "GiBps_output": round(gib(n * 4, wd), 2),
                                "kernel_ms": round(dk, 4), "max_abs_err": float((back - x).abs().max()),
+                               "steady_ms": steady_ms(ctx, lambda: codec.decode(e16, out=back, stream=st), st),
                                "decode_roofline": roof(n * 2, n * 4, dk, "k_decode_fixed1d_np<64, 16>", basis="write")}
     del enc16, e16, back, x
     torch.cuda.empty_cache()
@@ -533,9 +547,12 @@ def leg_configs(ctx):
         d_ms, dper = timed(ctx, lambda: codec.decode(e, out=back, stream=st), 5, 20, stream=st)
         dk = sum(dper) / len(dper)
         err = float((back - f).abs().max())
+        es = steady_ms(ctx, lambda: enc(f, st), st)
+        ds = steady_ms(ctx, lambda: codec.decode(e, out=back, stream=st), st)
         kn = "k_encode3d_fixed" if stride == 0 else "k_count3d + k_scan_ranges + k_encode3d_var"
         out[name] = {"encode_ms": round(k_ms, 4), "encode_GiBps_input": round(gib(nbytes, k_ms), 2),
                      "decode_ms": round(dk, 4), "decode_GiBps_output": round(gib(nbytes, dk), 2),
+                     "encode_steady_ms": es, "decode_steady_ms": ds,
                      "bits_per_value": round(cbits / f.numel(), 3), "max_abs_err": err,
                      "encode_roofline": roof(nbytes, cbits / 8, k_ms, kn),
                      "decode_roofline": roof(cbits / 8, nbytes, dk, "k_decode3d_fixed" if stride == 0 else
@@ -578,8 +595,11 @@ def leg_configs(ctx):
         back_b = torch.empty(n, dtype=torch.bfloat16, device=ctx.dev)
         _, bper = timed(ctx, lambda: codec.decode(e, out=back_b, stream=st), 5, 20, stream=st)
         bk = sum(bper) / len(bper)
+        es = steady_ms(ctx, lambda: enc(xb, st), st)
+        ds = steady_ms(ctx, lambda: codec.decode(e, out=back, stream=st), st)
         del back_b
         out[name] = {"encode_ms": round(k_ms, 4), "encode_GiBps_input": round(gib(n * 2, k_ms), 2),
+                     "encode_steady_ms": es, "decode_steady_ms": ds,
                      "bits_per_value": round(cbits / n, 3), "encode_roofline": er,
                      "decode_ms": round(dk, 4), "decode_GiBps_output": round(gib(n * 4, dk), 2),
                      "decode_roofline": dr,
