@@ -66,12 +66,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // (LdsWriter); otherwise every block writes exactly its length and the unclipped OrWriter is used.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane)
 {
+#if GCOW_DPP_SCAN
+  (void)lane;
+  return wave_incl_scan_dpp(x);
+#else
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(x, o, 64);
     x += lane >= (uint32_t)o ? y : 0u;
   }
   return x;
+#endif
 }
 
 template <int DT>
@@ -88,8 +93,7 @@ __global__ __launch_bounds__(64) void k_count3d(FieldDesc F, Params p, uint64_t*
     len = block_length<64>(h, u, p);
     lens[b] = (uint16_t)len;  // <= 9 + 64 * 33 bits
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) len += __shfl_xor(len, o, 64);
+  len = wave_sum_dpp(len);
   if (threadIdx.x == 0) sums[blockIdx.x] = len;
 }
 
@@ -113,7 +117,7 @@ __global__ __launch_bounds__(64) void k_encode3d_var(FieldDesc F, Params p, cons
   // placement first (lengths from the count pass), so the 64 coefficients are live only from gather to code
   const uint32_t len = valid ? lens[b] : 0u;
   const uint32_t incl = wave_incl_scan(len, lane);
-  const uint32_t excl = incl - len, total = __shfl(incl, 63, 64);
+  const uint32_t excl = incl - len, total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   const uint64_t base = rbase[blockIdx.x];
   const uint32_t lb = (uint32_t)(base & 31);
   const uint32_t W = (lb + total + 31) >> 5;

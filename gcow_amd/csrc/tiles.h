@@ -10,16 +10,51 @@
 namespace gcow {
 
 // ------------------------------------------------------------------------------------------------ tiles
-template <uint32_t T>
+#ifndef GCOW_DPP_SCAN
+#define GCOW_DPP_SCAN 1
+#endif
+// Inclusive wave prefix sum through DPP moves (no LDS round trip per step, as __shfl_up's ds_bpermute takes): sums
+// within rows of 16 lanes by row_shr 1, 2, 4, 8 (lanes shifted in from outside the row read 0), then row 15's total
+// into rows 1 and 3 (row_bcast:15) and lane 31's into rows 2 and 3 (row_bcast:31).
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x)
+{
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+// Sum over the wave (wave-uniform), through the DPP prefix sum
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t x)
+{
+#if GCOW_DPP_SCAN
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_dpp(x), 63);
+#else
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+#endif
+}
+
+// Exclusive prefix sum over the workgroup. GUARD: a trailing barrier so that `sh` can be reused at once; a caller
+// that passes a barrier of its own before the next use of `sh` drops it.
+template <uint32_t T, bool GUARD = true>
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* total, uint32_t* sh)
 {
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   uint32_t x = v;
+#if GCOW_DPP_SCAN
+  x = wave_incl_scan_dpp(x);
+#else
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     uint32_t y = __shfl_up(x, o, 64);
     if (lane >= (uint32_t)o) x += y;
   }
+#endif
   if (T > 64) {
     if (lane == 63) sh[wid] = x;
     __syncthreads();
@@ -30,11 +65,11 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* t
       off += w < wid ? s : 0u;
       tot += s;
     }
-    __syncthreads();
+    if (GUARD || !GCOW_DPP_SCAN) __syncthreads();
     *total = tot;
     return off + x - v;
   } else {
-    *total = __shfl(x, 63, 64);
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
     return x - v;
   }
 }

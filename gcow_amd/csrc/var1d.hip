@@ -660,8 +660,7 @@ __global__ __launch_bounds__(V1T) void k_count1d_var_tile(FieldDesc F, Params p,
       }
       uint32_t lsum;
       packed[i] = v1_count_tile<DT, true>(F, p, cur, t0 + i, lsum);
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
+      lsum = wave_sum_dpp(lsum);
       if ((tid & 63u) == 0) red[i][tid >> 6] = lsum;
     }
   } else {  // partial tiles, the padded last block, strided or unaligned input
@@ -674,8 +673,7 @@ __global__ __launch_bounds__(V1T) void k_count1d_var_tile(FieldDesc F, Params p,
         raw.load(F, t0 + i, wide_ok);
         packed[i] = v1_count_tile<DT>(F, p, raw, t0 + i, lsum);
       }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o, 64);
+      lsum = wave_sum_dpp(lsum);
       if ((tid & 63u) == 0) red[i][tid >> 6] = lsum;
     }
   }
@@ -718,7 +716,7 @@ __device__ __forceinline__ void v1_tile_code(const FieldDesc& F, const Params& p
     lsum += len[k];
   }
   uint32_t tot_unused;
-  const uint32_t excl = lb + block_exclusive_scan<V1T>(lsum, &tot_unused, scan_sh);
+  const uint32_t excl = lb + block_exclusive_scan<V1T, false>(lsum, &tot_unused, scan_sh);  // barrier below
   if (lsum) {  // the two words this lane shares with its neighbours start at zero
     win[excl >> 6] = 0ull;
     win[(excl + lsum - 1) >> 6] = 0ull;
