@@ -553,6 +553,9 @@ hipError_t launch_encode1d_var_sp(const FieldDesc& F, const Params& p, uint32_t*
 //   k_encode1d_var_tile_big  the same body with the worst-case window (140 bits per block), a grid-stride loop over
 //                        the list of oversized tiles k_encode1d_var_tile appended to (the count kernel empties it).
 constexpr uint32_t V1CT = 8;                                      // tiles per count workgroup
+#ifndef V1_COUNT_PF
+#define V1_COUNT_PF 1  // tiles of loads in flight ahead of the counted one (k_count1d_var_tile), 1 .. 3
+#endif
 constexpr uint32_t V1QS = 1500;                                   // small window, qwords
 constexpr uint32_t V1TAB = 1024;                                  // pair-table rows 0..3 in LDS
 
@@ -588,6 +591,18 @@ __device__ __forceinline__ void v1_wait_n(v1_u4 (&w)[NL])
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(w[0]), "+v"(w[1]) : "n"(N) : "memory");
   else
     asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : "n"(N) : "memory");
+}
+
+// the same for k tiles of NL loads each still in flight (k folds to a constant in the unrolled tile loop)
+template <int NL>
+__device__ __forceinline__ void v1_wait_tiles(v1_u4 (&w)[NL], uint32_t k)
+{
+  switch (k) {
+    case 0: v1_wait_n<0>(w); break;
+    case 1: v1_wait_n<NL>(w); break;
+    case 2: v1_wait_n<2 * NL>(w); break;
+    default: v1_wait_n<3 * NL>(w); break;
+  }
 }
 
 // One tile's block lengths (bytes packed per lane) and the lane's sum. FULL: every block of the tile is inside the
@@ -640,22 +655,25 @@ __global__ __launch_bounds__(V1T) void k_count1d_var_tile(FieldDesc F, Params p,
   uint32_t packed[V1CT];
   if (wide_ok && (uint64_t)(t0 + V1CT) * V1TILE <= F.n[0] / 4) {
     const v1_v4i rs = v1_rsrc((const char*)F.data + (size_t)t0 * TB, V1CT * TB);
-    v1_u4 buf[2][NL];
+    // a ring of PF + 1 tiles: tile i + PF is requested before tile i is counted, so PF tiles of loads stay in flight
+    constexpr uint32_t PF = V1_COUNT_PF, RING = PF + 1;
+    v1_u4 buf[RING][NL];
 #pragma unroll
-    for (int h = 0; h < NL; h++) buf[0][h] = v1_ld16((tid * NL + h) * 16u, rs);
+    for (uint32_t i = 0; i < PF && i < V1CT; i++)
+#pragma unroll
+      for (int h = 0; h < NL; h++) buf[i][h] = v1_ld16(i * TB + (tid * NL + h) * 16u, rs);
 #pragma unroll
     for (uint32_t i = 0; i < V1CT; i++) {
-      if (i + 1 < V1CT) {
+      if (i + PF < V1CT) {
 #pragma unroll
-        for (int h = 0; h < NL; h++) buf[(i + 1) & 1][h] = v1_ld16((i + 1) * TB + (tid * NL + h) * 16u, rs);
-        v1_wait_n<NL>(buf[i & 1]);
-      } else {
-        v1_wait_n<0>(buf[i & 1]);
+        for (int h = 0; h < NL; h++) buf[(i + PF) % RING][h] = v1_ld16((i + PF) * TB + (tid * NL + h) * 16u, rs);
       }
+      // loads issued after tile i's: those of tiles i + 1 .. min(i + PF, V1CT - 1)
+      v1_wait_tiles<NL>(buf[i % RING], (i + PF < V1CT ? PF : V1CT - 1 - i));
       V1Raw<DT> cur;
 #pragma unroll
       for (int h = 0; h < NL; h++) {
-        const v1_u4 v = buf[i & 1][h];
+        const v1_u4 v = buf[i % RING][h];
         cur.w[h] = make_uint4(v.x, v.y, v.z, v.w);
       }
       uint32_t lsum;
