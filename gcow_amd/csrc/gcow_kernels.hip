@@ -1368,6 +1368,9 @@ __device__ __forceinline__ void decode_block1d_fast(uint64_t w, const uint16_t* 
 #ifndef GCOW_DEC_PAIR
 #define GCOW_DEC_PAIR 1
 #endif
+#ifndef GCOW_DEC_PAIR2
+#define GCOW_DEC_PAIR2 1  // decode_block1d_pair: select-free steps (budget / window overruns only flag the block special)
+#endif
 // ---- two planes per lookup (64-bit blocks). The group phase lasts 1.5 planes on average on gradient-like data but
 // the wave-uniform loop above runs the wave's maximum (4.6 planes: profiles/r04_dec_pair_table.log), so each step
 // here decodes as many of the next two planes as the next 10 stream bits determine, and lanes step on their own.
@@ -1413,6 +1416,27 @@ __device__ __forceinline__ void decode_block1d_pair(uint64_t w, const uint32_t* 
   uint64_t Y = 0;
   uint32_t n = 0;
   int j = 0;
+#if GCOW_DEC_PAIR2
+  // Every step takes the entry's two-plane fields (which fall back to the first plane's when the second is not
+  // decoded within the 10 bits), with no per-step budget or window selects; what they would have guarded only makes
+  // the block special: a plane code crossing the 64-bit budget leaves pos > 64, and a step from nibble 15 (j ends at
+  // 17) consumed plane M0 - 16, which belongs to the second window. A second plane below plane 0 (a step from j = M0)
+  // lands past the coefficients' low bit and is shifted out by window_to_coeffs; its length only matters for pos > 64.
+  const int jm = min(M0, 15);
+#pragma unroll
+  for (int it = 0; it < 16; it++) {
+    const bool act = n < 3 && pos < 64u && j <= jm;
+    if (!__any(act)) break;
+    if (act) {
+      const uint32_t e = dtp[(n << 10) | ((uint32_t)(w >> pos) & 1023u)];
+      Y |= (uint64_t)(e & 255u) << (4 * j);
+      pos += (e >> 12) & 15u;
+      n = (e >> 18) & 3u;
+      j += 1 + (int)((e >> 20) & 1u);
+    }
+  }
+  special = (M0 >= 0 && pos > 64u) || j == 17 || (n < 3 && pos < 64u && j <= M0);
+#else
   bool cross = false;
 #pragma unroll
   for (int it = 0; it < 16; it++) {
@@ -1433,6 +1457,7 @@ __device__ __forceinline__ void decode_block1d_pair(uint64_t w, const uint32_t* 
     }
   }
   special = cross || (n < 3 && pos < 64u && j <= M0);  // budget inside a group plane, or a group phase past 16 planes
+#endif
   if (j < 16 && pos < 64u) Y |= (w >> pos) << (4 * j);  // verbatim nibbles (bits past the word are zero)
   uint32_t u[4] = {0, 0, 0, 0};
   if (M0 >= 0) {
