@@ -65,6 +65,49 @@ def window_to_coeffs(Y, top, u):
         u[i] |= bitrev32(field) >> (31 - top)
 
 
+def gather_tab():  # gcow_kernels.hip make_gather_tab
+    T = [0] * 1024
+    for s in range(4):
+        for b in range(256):
+            r = 0
+            for i in range(4):
+                r |= ((b >> i) & 1) << (8 * i + 7 - 2 * s)
+                r |= ((b >> (4 + i)) & 1) << (8 * i + 6 - 2 * s)
+            T[256 * s + b] = r
+    return T
+
+
+GT = gather_tab()
+
+
+def perm_b32(s0, s1, sel):  # v_perm_b32 for selector bytes 0..7 and 0x0c (zero)
+    src = [(s1 >> (8 * k)) & 255 for k in range(4)] + [(s0 >> (8 * k)) & 255 for k in range(4)]
+    out = 0
+    for k in range(4):
+        c = (sel >> (8 * k)) & 255
+        out |= (src[c] if c < 8 else 0) << (8 * k)
+    return out
+
+
+def window_to_coeffs_lds(Y, top, u):  # gcow_kernels.hip window_to_coeffs_lds
+    lo, hi = Y & 0xFFFFFFFF, Y >> 32
+    A = GT[lo & 255] | GT[256 + ((lo >> 8) & 255)] | GT[512 + ((lo >> 16) & 255)] | GT[768 + (lo >> 24)]
+    B = GT[hi & 255] | GT[256 + ((hi >> 8) & 255)] | GT[512 + ((hi >> 16) & 255)] | GT[768 + (hi >> 24)]
+    for i in range(4):
+        u[i] |= perm_b32(A, B, ((4 + i) << 24) | (i << 16) | 0x0C0C) >> (31 - top)
+
+
+def test_gather_window_matches_transpose():
+    rng = np.random.default_rng(9)
+    for _ in range(3000):
+        Y = int(rng.integers(0, 2 ** 63)) * 2 + int(rng.integers(0, 2))
+        top = int(rng.integers(0, 32))
+        a, b = [0] * 4, [0] * 4
+        window_to_coeffs(Y, top, a)
+        window_to_coeffs_lds(Y, top, b)
+        assert a == b, (hex(Y), top, a, b)
+
+
 def i32(v):
     v &= 0xFFFFFFFF
     return v - (1 << 32) if v >> 31 else v
