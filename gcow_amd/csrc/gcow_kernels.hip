@@ -1466,7 +1466,13 @@ __device__ __forceinline__ void decode_block1d_pair(uint64_t w, const uint32_t* 
 {
   const bool nonzero = w & 1u;
   const int emax = (int)((w >> 1) & 255u) - 127;
+#if GCOW_DEC_PAIR2
+  // header bit 0: +0 whatever follows -- taken as a block whose planes are all empty (u = 0, so every value is
+  // sc * 0 = +0 with sc >= 0), not selected per value at the end
+  const uint64_t r = nonzero ? w >> 9 : 0ull;
+#else
   const uint64_t r = w >> 9;
+#endif
   const int z = r ? (int)__builtin_ctzll(r) : 64;
   const int M0 = 31 - z;  // < 0: every coded plane empty
   uint32_t pos = 9u + (uint32_t)z;
@@ -1482,8 +1488,9 @@ __device__ __forceinline__ void decode_block1d_pair(uint64_t w, const uint32_t* 
   const int jm = min(M0, 15);
 #pragma unroll
   for (int it = 0; it < 16; it++) {
-    const bool act = n < 3 && pos < 64u && j <= jm;
-    if (!__any(act)) break;
+    // the first step is every lane with a coded plane (n = 0, j = 0, pos <= 40): no wave vote
+    const bool act = it == 0 ? M0 >= 0 : n < 3 && pos < 64u && j <= jm;
+    if (it > 0 && !__any(act)) break;
     if (act) {
       const uint32_t e = dtp[(n << 10) | ((uint32_t)(w >> pos) & 1023u)];
       Y |= (uint64_t)(e & 255u) << (4 * j);
@@ -1534,8 +1541,13 @@ __device__ __forceinline__ void decode_block1d_pair(uint64_t w, const uint32_t* 
   for (int i = 0; i < 4; i++) q[i] = (int32_t)((u[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
   inv_lift(q[0], q[1], q[2], q[3]);
   const float sc = dequant_scale(emax);
+#if GCOW_DEC_PAIR2
+#pragma unroll
+  for (int i = 0; i < 4; i++) f[i] = sc * (float)q[i];  // header bit 0: q = 0 above
+#else
 #pragma unroll
   for (int i = 0; i < 4; i++) f[i] = nonzero ? sc * (float)q[i] : 0.0f;  // header bit 0: +0 whatever follows
+#endif
 }
 
 template <uint32_t WB> struct PipeWord;

@@ -135,14 +135,14 @@ def fast_pair(w, new):
     """decode_block1d_pair's fast path for one 64-bit block: (special, 4 float32 bit patterns)."""
     nonzero = w & 1
     emax = ((w >> 1) & 255) - 127
-    r = w >> 9
+    r = (w >> 9) if (nonzero or not new) else 0  # pair2: a zero header bit is a block of empty planes
     z = (r & -r).bit_length() - 1 if r else 64
     M0 = 31 - z
     pos, Y, n, j = 9 + z, 0, 0, 0
     if new:
         jm = min(M0, 15)
-        for _ in range(16):
-            if not (n < 3 and pos < 64 and j <= jm):
+        for it in range(16):
+            if not ((M0 >= 0) if it == 0 else (n < 3 and pos < 64 and j <= jm)):
                 break
             e = TAB[(n << 10) | ((w >> pos) & 1023)]
             Y = (Y | ((e & 255) << (4 * j))) & M64
@@ -177,7 +177,10 @@ def fast_pair(w, new):
     q = [i32((v ^ NB) - NB) for v in u]
     q = inv_lift(*q)
     sc = dequant_scale(emax)
-    f = np.array([sc * np.float32(v) if nonzero else np.float32(0.0) for v in q], np.float32)
+    if new:  # q = 0 for a zero header bit: sc * 0 = +0
+        f = np.array([sc * np.float32(v) for v in q], np.float32)
+    else:
+        f = np.array([sc * np.float32(v) if nonzero else np.float32(0.0) for v in q], np.float32)
     return special, f.view(np.uint32)
 
 
