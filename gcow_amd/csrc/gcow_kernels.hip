@@ -1499,7 +1499,11 @@ __device__ __forceinline__ void decode_block1d_pair(uint64_t w, const uint32_t* 
       j += 1 + (int)((e >> 20) & 1u);
     }
   }
-  special = (M0 >= 0 && pos > 64u) || j == 17 || (n < 3 && pos < 64u && j <= M0);
+  // special: a plane code crossed the budget, or the steps reached nibble 16 (a group phase as long as the window, or
+  // a step from nibble 15 that consumed plane M0 - 16; a group phase that ended exactly at nibble 16 is decoded
+  // generically too, which only costs time). Otherwise every coded plane is in Y: the loop stopped with n >= 3, with
+  // the budget used up (pos = 64), or past plane 0.
+  special = M0 >= 0 && (pos > 64u || j >= 16);
 #else
   bool cross = false;
 #pragma unroll
@@ -1522,7 +1526,13 @@ __device__ __forceinline__ void decode_block1d_pair(uint64_t w, const uint32_t* 
   }
   special = cross || (n < 3 && pos < 64u && j <= M0);  // budget inside a group plane, or a group phase past 16 planes
 #endif
+#if GCOW_DEC_PAIR2
+  // verbatim nibbles (bits past the word are zero): pos >= 9, so the two-step shift gives 0 at pos = 64; lanes with
+  // pos > 64 or j >= 16 are special and their Y is not used
+  Y |= ((w >> (pos - 1u)) >> 1) << (4 * j);
+#else
   if (j < 16 && pos < 64u) Y |= (w >> pos) << (4 * j);  // verbatim nibbles (bits past the word are zero)
+#endif
   uint32_t u[4] = {0, 0, 0, 0};
   if (M0 >= 0) {
     if constexpr (GATHER) window_to_coeffs_lds(dtp + 3 * 1024, Y, M0, u);
@@ -1540,11 +1550,15 @@ __device__ __forceinline__ void decode_block1d_pair(uint64_t w, const uint32_t* 
 #pragma unroll
   for (int i = 0; i < 4; i++) q[i] = (int32_t)((u[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
   inv_lift(q[0], q[1], q[2], q[3]);
-  const float sc = dequant_scale(emax);
 #if GCOW_DEC_PAIR2
+  // (float)q * 2^(emax - 30) as one v_ldexp_f32 per value: the product by the exact power of two that dequant_scale
+  // gives, rounded once alike (denormal results included); below 2^-149 dequant_scale's 0 gives a signed zero, which
+  // the ldexp gives at any exponent under -181 (|q| < 2^31)
+  const int e = emax - 30 < -149 ? -256 : emax - 30;
 #pragma unroll
-  for (int i = 0; i < 4; i++) f[i] = sc * (float)q[i];  // header bit 0: q = 0 above
+  for (int i = 0; i < 4; i++) f[i] = __builtin_amdgcn_ldexpf((float)q[i], e);  // header bit 0: q = 0 above
 #else
+  const float sc = dequant_scale(emax);
 #pragma unroll
   for (int i = 0; i < 4; i++) f[i] = nonzero ? sc * (float)q[i] : 0.0f;  // header bit 0: +0 whatever follows
 #endif

@@ -149,7 +149,7 @@ def fast_pair(w, new):
             pos += (e >> 12) & 15
             n = (e >> 18) & 3
             j += 1 + ((e >> 20) & 1)
-        special = (M0 >= 0 and pos > 64) or j == 17 or (n < 3 and pos < 64 and j <= M0)
+        special = M0 >= 0 and (pos > 64 or j >= 16)
     else:
         cross = False
         for _ in range(16):
@@ -166,7 +166,9 @@ def fast_pair(w, new):
                 n = (e >> (18 if two else 16)) & 3
                 j += 2 if two else 1
         special = cross or (n < 3 and pos < 64 and j <= M0)
-    if j < 16 and pos < 64:
+    if new:  # unconditional: 0 at pos = 64; lanes with pos > 64 or j >= 16 are special
+        Y = (Y | ((((w >> (pos - 1)) >> 1) << (4 * (j & 15))) & M64)) & M64 if j < 16 else Y
+    elif j < 16 and pos < 64:
         Y = (Y | ((w >> pos) << (4 * j))) & M64
     u = [0, 0, 0, 0]
     if M0 >= 0:
@@ -177,8 +179,9 @@ def fast_pair(w, new):
     q = [i32((v ^ NB) - NB) for v in u]
     q = inv_lift(*q)
     sc = dequant_scale(emax)
-    if new:  # q = 0 for a zero header bit: sc * 0 = +0
-        f = np.array([sc * np.float32(v) for v in q], np.float32)
+    if new:  # q = 0 for a zero header bit; one ldexp per value, exponents under -149 as -256 (a signed zero)
+        e = emax - 30 if emax - 30 >= -149 else -256
+        f = np.array([np.ldexp(np.float32(v), e) for v in q], np.float32)
     else:
         f = np.array([sc * np.float32(v) if nonzero else np.float32(0.0) for v in q], np.float32)
     return special, f.view(np.uint32)
@@ -193,6 +196,9 @@ def _blocks(orc):
     sparse = np.zeros(4 * 2000, np.float32)
     sparse[rng.integers(0, sparse.size, 1500)] = rng.standard_normal(1500).astype(np.float32)
     vals.append(sparse)
+    small = rng.standard_normal(4 * 1500).astype(np.float32)
+    small *= np.float32(2.0) ** rng.integers(-128, -100, small.size).astype(np.float32)  # scales 2^-158 .. 2^-130
+    vals.append(small)
     a = np.concatenate(vals)
     words, _ = orc.compress(a, orc.rate(16, 1))
     arb = rng.integers(0, 2 ** 63, 4000, dtype=np.int64).astype(np.uint64) * np.uint64(2) + \
