@@ -1891,9 +1891,9 @@ __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& p
 #pragma unroll
   for (int i = 0; i < 4; i++) q[i] = (int32_t)((u[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
   inv_lift(q[0], q[1], q[2], q[3]);
-  const float sc = dequant_scale(emax);
+  const int e = emax - 30 < -149 ? -256 : emax - 30;  // as decode_block1d_pair: ldexp = dequant_scale(emax) * q
 #pragma unroll
-  for (int i = 0; i < 4; i++) f[i] = sc * (float)q[i];
+  for (int i = 0; i < 4; i++) f[i] = __builtin_amdgcn_ldexpf((float)q[i], e);
   return true;
 }
 
