@@ -2313,6 +2313,24 @@ __global__ __launch_bounds__(256) void k_stitch_shards(uint64_t* __restrict__ ds
 }
 
 // ------------------------------------------------------------------------------------------------ decode + mean
+// acc / nstreams for the N sums of a lane: an IEEE division, or -- nstreams a power of two (the usual world size) --
+// the product by the exact reciprocal, which is the same correctly rounded value of the same quotient (a uniform
+// branch: the division's expansion runs only for other world sizes).
+template <int N>
+__device__ __forceinline__ void mean_scale(float* a, uint32_t nstreams)
+{
+#pragma clang fp contract(off)
+  if ((nstreams & (nstreams - 1u)) == 0u) {
+    const float inv = 1.0f / (float)nstreams;
+#pragma unroll
+    for (int i = 0; i < N; i++) a[i] = a[i] * inv;
+  } else {
+    const float nf = (float)nstreams;
+#pragma unroll
+    for (int i = 0; i < N; i++) a[i] = a[i] / nf;
+  }
+}
+
 // The receive side of the compressed all-gather hook: nstreams 1-D streams of the same shape
 // (one per rank, stream_words apart) are decoded and averaged in one launch instead of one decode and one add per
 // rank. Each lane accumulates in fp32 in rank order, acc = ((0 + x_0) + x_1) + ..., then stores acc / nstreams: the
@@ -2346,9 +2364,7 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d(FieldDesc F, Params
 #pragma unroll
     for (int i = 0; i < 4; i++) acc[i] = acc[i] + f[i];
   }
-  const float nf = (float)nstreams;
-#pragma unroll
-  for (int i = 0; i < 4; i++) acc[i] = acc[i] / nf;
+  mean_scale<4>(acc, nstreams);
   store_block1d(F, b, acc);
 }
 
@@ -2449,7 +2465,7 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
       }
     }
   }
-  const float nf = (float)nstreams;
+  mean_scale<U * 4>(&acc[0][0], nstreams);
   float* out = (float*)F.data;
 #pragma unroll
   for (int k = 0; k < U; k++) {
@@ -2457,7 +2473,7 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
     if (b < nfull) {
       float v[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) v[i] = acc[k][i] / nf;
+      for (int i = 0; i < 4; i++) v[i] = acc[k][i];
       if (F.vec && F.dtype != DT_BF16) *(float4*)(out + 4 * (uint64_t)b) = make_float4(v[0], v[1], v[2], v[3]);
       else store_block1d(F, b, v);
     }
@@ -2531,7 +2547,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_
       }
     }
   }
-  const float nf = (float)nstreams;
+  const float nf = (float)nstreams;  // a plain division here: the two-path mean_scale costs this kernel registers (+4 %)
   const uint32_t lane = tid & 63u, m = lane & 7u;
   float4* o4 = (float4*)F.data + (c - m) * 16 + m;
   uint2* o2 = (uint2*)F.data + (c - m) * 16 + m;  // bf16 output: 8 bytes per block, a chunk is one 128-byte line
@@ -2612,7 +2628,7 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
     }
   }
   if (c >= nchunks) return;
-  const float nf = (float)nstreams;
+  mean_scale<64>(&acc[0][0], nstreams);
   float* out = (float*)F.data;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
@@ -2620,7 +2636,7 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
     if (b < b1) {
       float v[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) v[i] = acc[k][i] / nf;
+      for (int i = 0; i < 4; i++) v[i] = acc[k][i];
       if (F.vec && F.dtype != DT_BF16 && 4 * b + 4 <= F.n[0]) *(float4*)(out + 4 * b) = make_float4(v[0], v[1], v[2], v[3]);
       else store_block1d(F, b, v);
     }
@@ -2654,13 +2670,13 @@ __global__ __launch_bounds__(256) void k_decode_mean1d_generic(FieldDesc F, Para
       }
     }
   }
-  const float nf = (float)nstreams;
+  mean_scale<64>(&acc[0][0], nstreams);
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     if (b0 + k < b1) {
       float v[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) v[i] = acc[k][i] / nf;
+      for (int i = 0; i < 4; i++) v[i] = acc[k][i];
       store_block1d(F, b0 + k, v);
     }
   }
