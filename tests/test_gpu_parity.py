@@ -710,7 +710,13 @@ def test_fast1d_decode_arbitrary_streams(gc, orc, r):
     w = rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64) * np.uint64(2) + rng.integers(0, 2, nw).astype(np.uint64)
     # sparse words: long zero runs after the header
     sparse = w & (rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64) & rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64))
-    words = np.concatenate([w, sparse | np.uint64(0x0101010101010101)])
+    # very sparse words (one bit in eight after the header): group phases past the 16-plane window, plane codes that
+    # cross the budget, steps from the window's last nibble -- the pair decoder's special blocks
+    dense8 = np.zeros(nw, np.uint64)
+    for _ in range(3):
+        dense8 |= rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64)
+    very = (~dense8 & rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64)) | np.uint64(1)
+    words = np.concatenate([w, sparse | np.uint64(0x0101010101010101), very])
     n = words.size * 64 // r
     op = orc.rate(r, 1)
     ref = orc.decompress(words, (n,), op)
@@ -718,6 +724,36 @@ def test_fast1d_decode_arbitrary_streams(gc, orc, r):
                   P(gc, op))
     torch.cuda.synchronize()
     assert np.array_equal(d.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_decode_mean_arbitrary_streams(gc, orc, world):
+    """decode_mean (the fixed-rate pair decoder with gather tables, and its special blocks) on arbitrary and very
+    sparse 64-bit words: the fp32 mean, in rank order, of the oracle's decode of each stream (a power-of-two world
+    scales by the reciprocal, the other divides)."""
+    rng = np.random.default_rng(40 + world)
+    nw = 1 << 15
+    streams = []
+    for r in range(world):
+        w = rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64) * np.uint64(2) + rng.integers(0, 2, nw).astype(np.uint64)
+        d8 = np.zeros(nw, np.uint64)
+        for _ in range(3):
+            d8 |= rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64)
+        very = (~d8 & rng.integers(0, 2 ** 63, nw, dtype=np.int64).view(np.uint64)) | np.uint64(1)
+        streams.append(np.where(rng.random(nw) < 0.5, w, very))
+    n = nw * 4
+    op = orc.rate(16, 1)
+    acc = np.zeros(n, np.float32)
+    with np.errstate(over="ignore", invalid="ignore"):  # arbitrary headers decode to +-inf; inf - inf is NaN
+        for st in streams:
+            acc = acc + orc.decompress(np.concatenate([st, np.zeros(2, np.uint64)]), (n,), op)
+        want = acc / np.float32(world)
+    buf = torch.from_numpy(np.concatenate(streams + [np.zeros(2, np.uint64)]).view(np.int64)).cuda()
+    got = gc.decode_mean(buf, nw, world, n, P(gc, op)).cpu().numpy()
+    # inf + -inf: a NaN whose bit pattern is the device's (x86 and the GPU differ in the default NaN's sign)
+    nan = np.isnan(want)
+    assert np.array_equal(np.isnan(got), nan)
+    assert np.array_equal(got[~nan].view(np.uint32), want[~nan].view(np.uint32))
 
 
 @pytest.mark.parametrize("params", [(64, 64, 20, -1074), (64, 64, 64, -100), (32, 32, 12, -1074), (32, 32, 64, -60)])
