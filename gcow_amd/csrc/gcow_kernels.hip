@@ -213,6 +213,10 @@ __device__ __forceinline__ uint64_t encode_block1d_lean5(const float* f, const u
   return WB == 64 ? acc : (acc & ((1ull << WB) - 1ull));
 }
 
+#ifndef GCOW_C2_PAIR1_ALWAYS
+#define GCOW_C2_PAIR1_ALWAYS 1  // lean-6: the second pair step without a wave vote
+#endif
+
 // Lean-6 block: the lean-5 stream (encode.c:457-495 for d = 1, fixed rate, kmin = 0) with
 //  * the block maximum as a float max3 of |f| (NaN caught by two unordered compares: it never wins the maximum,
 //    encode.c:146-150, but it casts to INT_MIN, so such blocks take the generic coder);
@@ -252,6 +256,14 @@ __device__ __forceinline__ uint64_t encode_block1d_lean6(const float* f, const u
   uint32_t pos = 9 + sh;
   uint32_t e = tab[(uint32_t)Y & 255u];
   uint32_t G = e >> 17, gl = (e >> 13) & 15u;
+#if GCOW_C2_PAIR1_ALWAYS
+  // pair 1 for every lane, no wave vote (~92 % of waves take it anyway): past a lane's group phase the table's rows
+  // n >= 3 code planes 2 and 3 as their verbatim nibbles, the bits the verbatim run would give them
+  int j = 4;
+  e = tab5_next(tab, e, ((uint32_t)Y >> 8) & 255u);
+  G |= (e >> 17) << gl;
+  gl += (e >> 13) & 15u;
+#else
   int j = 2;
   if (__any(jg >= 2)) {
     e = tab5_next(tab, e, ((uint32_t)Y >> 8) & 255u);
@@ -259,6 +271,7 @@ __device__ __forceinline__ uint64_t encode_block1d_lean6(const float* f, const u
     gl += (e >> 13) & 15u;
     j = 4;
   }
+#endif
   const uint32_t hdr = m ? 2u * E + 3u : 0u;  // zero block: a single 0 bit, every later bit 0 as well
   uint64_t acc = (uint64_t)hdr | ((uint64_t)G << pos);
   pos += gl;
