@@ -1854,8 +1854,8 @@ __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& p
   const uint64_t w = lds_win64(sw, pos);
   const int emax = (int)((w >> 1) & 255u) - 127;
   const int np = min(32, min(maxprec, max(0, emax + cexp)));  // coded planes 31 .. 32 - np
-  const uint64_t r = w >> 9;
-  const int z = r ? (int)__builtin_ctzll(r) : 64;  // empty planes (any np <= 32 < 55 is covered)
+  // empty planes: ctz of the 55 bits after the header, a sentinel one at bit 55 for none (any np <= 32 < 55)
+  const int z = (int)__builtin_ctzll((w >> 9) | (1ull << 55));
   f[0] = f[1] = f[2] = f[3] = 0.0f;
   if (!(w & 1u)) {  // zero block (or no precision): one 0 bit
     pos += 1;
@@ -1887,10 +1887,10 @@ __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& p
   const uint32_t vpos = wbase + off;
   const uint32_t t = (uint32_t)(nbelow - j);  // verbatim planes, 4 bits each
   const uint32_t nb = 4u * t;                 // <= 128
+  // the run's window is not masked at nb: the next block's bits beyond it land on planes below kmin = 32 - np, which
+  // one mask of the coefficients clears
   uint64_t v0 = lds_win64(sw, vpos), v1 = 0;
   if (nb > 64) v1 = lds_win64(sw, vpos + 64);
-  if (nb < 64) v0 &= (1ull << nb) - 1ull;
-  else if (nb < 128) v1 &= (1ull << (nb - 64)) - 1ull;
   const uint32_t sft = 4u * (uint32_t)j;  // <= 32
   const uint64_t Ylo = (uint64_t)G | (v0 << sft);
   uint32_t u[4] = {0u, 0u, 0u, 0u};
@@ -1899,6 +1899,9 @@ __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& p
     const uint64_t Yhi = ((v0 >> 1) >> (63u - sft)) | (v1 << sft);
     window_to_coeffs(Yhi, M0 - 16, u);
   }
+  const uint32_t keep = ~0u << (uint32_t)(32 - np);  // planes 31 .. kmin (np >= 1 here)
+#pragma unroll
+  for (int i = 0; i < 4; i++) u[i] &= keep;
   pos = vpos + nb;
   int32_t q[4];
 #pragma unroll
