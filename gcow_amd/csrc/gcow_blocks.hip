@@ -47,7 +47,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   }
   __syncthreads();
   uint32_t* dst = out32 + (uint64_t)b0 * WPB;
-  for (uint32_t j = tid; j < nvalid * WPB; j += 256) dst[j] = lds_w[(j / WPB) * STRIDE + (j % WPB)];
+  bool wide = false;
+  if constexpr (WPB >= 4) {
+    wide = (((uintptr_t)out32) & 15u) == 0;
+    if (wide) {
+      // four stream words per thread and step: one 16-byte store (the rows' odd stride leaves four 4-byte LDS reads)
+      constexpr uint32_t Q = WPB / 4;
+      for (uint32_t j4 = tid; j4 < nvalid * Q; j4 += 256) {
+        const uint32_t* row = lds_w + (j4 / Q) * STRIDE + 4u * (j4 % Q);
+        ((uint4*)dst)[j4] = make_uint4(row[0], row[1], row[2], row[3]);
+      }
+    }
+  }
+  if (!wide)
+    for (uint32_t j = tid; j < nvalid * WPB; j += 256) dst[j] = lds_w[(j / WPB) * STRIDE + (j % WPB)];
   if (blockIdx.x == gridDim.x - 1 && tid == 0 && (((uint64_t)F.nblocks * WPB) & 1))
     out32[(uint64_t)F.nblocks * WPB] = 0u;  // stream_flush: zero-pad to a 64-bit boundary
 }
@@ -189,6 +202,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   const uint32_t b0 = blockIdx.x * 256u;
   const uint32_t nvalid = min(256u, F.nblocks - b0);
   const uint32_t* src = in32 + (uint64_t)b0 * WPB;
+  // word-wise: four words per thread and step (16-byte loads) measured 4 % slower here (r05_c3_wide_store_ab.log)
   for (uint32_t j = tid; j < nvalid * WPB; j += 256) lds_w[(j / WPB) * (WPB + 2) + (j % WPB)] = src[j];
   lds_w[tid * (WPB + 2) + WPB] = 0u;
   lds_w[tid * (WPB + 2) + WPB + 1] = 0u;
