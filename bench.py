@@ -396,7 +396,7 @@ def leg_hook_exchange(ctx, n):
     64 Ki values of the sharded result against the oracle's mean of every rank's decode."""
     import numpy as np
 
-    from gcow_amd import codec
+    from gcow_amd import codec, ddp
     from gcow_amd import dist as gdist
     W = ctx.world
     x = torch.empty(n, dtype=torch.float32, device=ctx.dev)
@@ -404,6 +404,9 @@ def leg_hook_exchange(ctx, n):
     out = {}
     for name, p, stride in (("rate16", codec.rate(16, 1), 0), ("acc1e-6", codec.accuracy(1e-6), 16)):
         enc = codec.Encoder((n,), torch.float32, p, ctx.dev, index_stride=stride)
+        # the sharded hook's own index spacing (ddp.SHARDED_INDEX_STRIDE); the stream words are the same
+        sstride = ddp.SHARDED_INDEX_STRIDE if stride else 0
+        senc = codec.Encoder((n,), torch.float32, p, ctx.dev, index_stride=sstride) if stride else enc
         ag = torch.empty(n, dtype=torch.float32, device=ctx.dev)
         sh = torch.empty(n, dtype=torch.float32, device=ctx.dev)
 
@@ -424,15 +427,15 @@ def leg_hook_exchange(ctx, n):
                 codec.decode_mean(g, nw, W, n, p, out=ag)
 
         def sharded_path():
-            e = enc(x)
+            e = senc(x)
             if stride:
-                pieces, pw, pidx, iw, lo, hi = gdist.shard_pieces_variable(e.words, e.bits_dev, e.index, n, stride)
+                pieces, pw, pidx, iw, lo, hi = gdist.shard_pieces_variable(e.words, e.bits_dev, e.index, n, sstride)
             else:
                 pieces, pw, lo, hi = gdist.shard_pieces_fixed(e.words, n, p.maxbits)
                 pidx, iw = None, 0
             shard = sh[lo:hi]
             if hi > lo:
-                codec.decode_mean(pieces, pw, W, hi - lo, p, pidx, iw, stride, out=shard)
+                codec.decode_mean(pieces, pw, W, hi - lo, p, pidx, iw, sstride, out=shard)
             gdist.allgather_shards(sh, shard, n)
 
         a_ms, _ = timed(ctx, allgather_path, 1, 4)
@@ -456,7 +459,7 @@ def leg_hook_exchange(ctx, n):
             del y
         out[name] = {"allgather_exchange_ms": round(a_ms, 4), "sharded_exchange_ms": round(s_ms, 4),
                      "sharded_equals_allgather": same, "sharded_mean_matches_oracle": ok}
-        del enc, ag, sh
+        del enc, senc, ag, sh
         torch.cuda.empty_cache()
     del x
     return out
@@ -640,14 +643,17 @@ def leg_decode_mean(ctx, W: int = 8):
     values (W different buckets of the bench distribution) decoded and averaged in one launch (codec.decode_mean), at
     rate 16 (the caller's default rate, hw/models/train_imagenet.py:155) and accuracy 1e-6 (the caller's default
     tolerance, :154). Roofline basis: the fp32 mean written; read + write adds the W compressed streams."""
-    from gcow_amd import codec
+    from gcow_amd import codec, ddp
     n = N_VALUES
     x = torch.empty(n, dtype=torch.float32, device=ctx.dev)
     mean = torch.empty_like(x)
     st = torch.cuda.current_stream(ctx.dev)
     res = {}
     for name, p, stride in (("rate16", codec.rate(16, 1), 0), ("acc1e-6", codec.accuracy(1e-6), 16)):
-        enc = codec.Encoder((n,), torch.float32, p, ctx.dev, index_stride=stride)
+        # variable rate: encoded with the sharded hook's index (every 8 blocks); the all-gather hook's index (every 16
+        # blocks) is every other entry of it -- the stream words do not depend on the spacing
+        sstride = ddp.SHARDED_INDEX_STRIDE if stride else 0
+        enc = codec.Encoder((n,), torch.float32, p, ctx.dev, index_stride=sstride)
         parts, idx, bits = [], [], 0
         for r in range(W):
             codec.fill_normal(x, 1e-3, seed=SEED + r, inject=True)
@@ -660,8 +666,10 @@ def leg_decode_mean(ctx, W: int = 8):
         buf = torch.zeros(W * sw + 2, dtype=torch.int64, device=ctx.dev)
         for r, t in enumerate(parts):
             buf[r * sw:r * sw + t.numel()] = t
-        ix = torch.cat(idx) if stride else None
-        ni = idx[0].numel() if stride else 0
+        ix8 = torch.cat(idx) if stride else None
+        ni8 = idx[0].numel() if stride else 0
+        ix = ix8.view(W, ni8)[:, ::stride // sstride].contiguous().view(-1) if stride else None
+        ni = ix.numel() // W if stride else 0
         del parts, idx, enc
         _, per = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ix, ni, stride, out=mean, stream=st), 3, 10,
                        stream=st)
@@ -669,15 +677,16 @@ def leg_decode_mean(ctx, W: int = 8):
         kname = "k_decode_mean_fixed1d<64>" if stride == 0 else "k_decode_mean1d_var<128>"
         # the sharded receive (ddp.compressed_sharded_hook): one rank's decode-mean of its 1/W shard from the W pieces
         # the all-to-all delivers (cut here from the same streams; the exchange itself is an N > 1 leg)
-        pieces, pw, pidx, iw, lo, hi = shard0_pieces(buf, sw, W, n, p, ix, ni)
+        pieces, pw, pidx, iw, lo, hi = shard0_pieces(buf, sw, W, n, p, ix8, ni8, sstride or 16)
         shard = mean[lo:hi]
-        _, sper = timed(ctx, lambda: codec.decode_mean(pieces, pw, W, hi - lo, p, pidx, iw, stride, out=shard,
+        _, sper = timed(ctx, lambda: codec.decode_mean(pieces, pw, W, hi - lo, p, pidx, iw, sstride, out=shard,
                                                        stream=st), 3, 10, stream=st)
         ks = sum(sper) / len(sper)
         res[name] = {"streams": W, "values": n, "kernel_ms": round(k, 4), "bits_per_value": round(bits / W / n, 3),
                      "roofline": roof(bits / 8, n * 4, k, kname, basis="write"),
-                     "sharded_receive_kernel_ms": round(ks, 4), "sharded_receive_values": hi - lo}
-        del buf, ix, pieces, pidx
+                     "sharded_receive_kernel_ms": round(ks, 4), "sharded_receive_values": hi - lo,
+                     "index_stride": stride, "sharded_index_stride": sstride}
+        del buf, ix, ix8, pieces, pidx
         torch.cuda.empty_cache()
     del x, mean
     return res

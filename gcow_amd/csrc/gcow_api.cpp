@@ -988,15 +988,17 @@ gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p
   if (streams_bytes / 8 < (uint64_t)nstreams * stream_words + 2)
     return fail(GCOW_ERR_INVALID, "stream buffer smaller than nstreams * stream_words + 2 words");
   if (p->minbits != p->maxbits) {
-    if (!d_index || index_stride != 16 || index_words < (F.nblocks + 15) / 16)
-      return fail(GCOW_ERR_INVALID, "variable-rate decode_mean needs each stream's index (stride 16)");
+    if (!d_index || (index_stride != 8 && index_stride != 16) ||
+        index_words < (F.nblocks + index_stride - 1) / index_stride)
+      return fail(GCOW_ERR_INVALID, "variable-rate decode_mean needs each stream's index (stride 8 or 16)");
   } else {
     if (d_index || index_stride || index_words)
       return fail(GCOW_ERR_INVALID, "fixed-rate decode_mean takes no block index (blocks are at b * maxbits)");
     if (stream_words < ((uint64_t)F.nblocks * p->maxbits + 63) / 64)
       return fail(GCOW_ERR_INVALID, "stream_words below one fixed-rate stream");
   }
-  GCOW_HIP(gcow::launch_decode_mean1d(F, P(*p), d_streams, stream_words, nstreams, d_index, index_words, hip_stream));
+  GCOW_HIP(gcow::launch_decode_mean1d(F, P(*p), d_streams, stream_words, nstreams, d_index, index_words, hip_stream,
+                                      index_stride ? index_stride : 16));
   return GCOW_OK;
 }
 

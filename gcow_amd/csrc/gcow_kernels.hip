@@ -2499,13 +2499,16 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
 #ifndef GCOW_DMV_WAVES
 #define GCOW_DMV_WAVES 4
 #endif
+#ifndef GCOW_DMV8_WAVES
+#define GCOW_DMV8_WAVES 5  // 8-block chunks: 32 sums per lane, 96 VGPRs (2 spilled) at 5 waves: 3.43 -> 3.05 ms (W = 8)
+#endif
 // Variable rate (1-D closed-form domain), the lean decoder's shape (k_decode1d_var_lean): LANES 16-block chunks per
 // workgroup; for each stream in rank order its span is staged in LDS (in 1, 2 or 4 parts, as there) and each lane
 // decodes its chunk into 64 registers of sums; the means leave through the 8 x 8 lane transposes as whole-line
 // stores. Complete workgroups only (whole chunks, full blocks, contiguous output); the launcher sends the rest to
 // k_decode_mean1d_var.
-template <uint32_t LANES, uint32_t CAPB>
-__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_WAVES, 8))) void k_decode_mean1d_var_lean(FieldDesc F, Params p,
+template <uint32_t LANES, uint32_t CAPB, uint32_t CH>
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(CH == 8 ? GCOW_DMV8_WAVES : GCOW_DMV_WAVES, 8))) void k_decode_mean1d_var_lean(FieldDesc F, Params p,
                                                                   const uint64_t* __restrict__ in,
                                                                   uint64_t stream_words,
                                                                   const uint64_t* __restrict__ index,
@@ -2513,8 +2516,8 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_
                                                                   uint32_t nstreams)
 {
 #pragma clang fp contract(off)
-  constexpr uint32_t CAP = LANES * 16 * CAPB / 64;
-  static_assert(LANES % 32 == 0 && CAP >= 32 * 16 * 140 / 64 + 4, "a quarter workgroup's longest span must fit");
+  constexpr uint32_t CAP = LANES * CH * CAPB / 64;
+  static_assert(LANES % 32 == 0 && CAP >= 32 * CH * 140 / 64 + 4 && CH % 8 == 0, "a quarter workgroup's longest span must fit");
   __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
   __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
   const uint32_t tid = threadIdx.x;
@@ -2523,9 +2526,9 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_
   const uint32_t* sw32 = (const uint32_t*)sw;
   const int cexp = 4 - p.minexp, maxprec = (int)min(p.maxprec, 64u);
   stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
-  float acc[16][4];
+  float acc[CH][4];
 #pragma unroll
-  for (int k = 0; k < 16; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
+  for (int k = 0; k < (int)CH; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
   for (uint32_t r = 0; r < nstreams; r++) {
     const uint64_t* sr = in + (uint64_t)r * stream_words;
     const uint64_t* ix = index + (uint64_t)r * index_words;
@@ -2550,7 +2553,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_
       if (tid / per != part) continue;
       uint32_t pos = (uint32_t)((int64_t)mine - 64 * w0);
 #pragma unroll
-      for (int k = 0; k < 16; k++) {
+      for (int k = 0; k < (int)CH; k++) {
         const uint32_t start = pos;
         float f[4];
         if (!dec_block1d_lean(sw32, pos, dt7, cexp, maxprec, f)) {
@@ -2565,11 +2568,11 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_
   }
   const float nf = (float)nstreams;  // a plain division here: the two-path mean_scale costs this kernel registers (+4 %)
   const uint32_t lane = tid & 63u, m = lane & 7u;
-  float4* o4 = (float4*)F.data + (c - m) * 16 + m;
-  uint2* o2 = (uint2*)F.data + (c - m) * 16 + m;  // bf16 output: 8 bytes per block, a chunk is one 128-byte line
+  float4* o4 = (float4*)F.data + (c - m) * CH + m;
+  uint2* o2 = (uint2*)F.data + (c - m) * CH + m;  // bf16 output: 8 bytes per block, a chunk is one 128-byte line
   const bool bf = F.dtype == DT_BF16;
 #pragma unroll
-  for (int rnd = 0; rnd < 2; rnd++) {
+  for (int rnd = 0; rnd < (int)CH / 8; rnd++) {
     float g[8][4];
 #pragma unroll
     for (int k = 0; k < 8; k++)
@@ -2581,10 +2584,10 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_
     if (bf) {
 #pragma unroll
       for (int i = 0; i < 8; i++)
-        o2[16 * i + 8 * rnd] = make_uint2(bf16x2_rne(g[i][0], g[i][1]), bf16x2_rne(g[i][2], g[i][3]));
+        o2[CH * i + 8 * rnd] = make_uint2(bf16x2_rne(g[i][0], g[i][1]), bf16x2_rne(g[i][2], g[i][3]));
     } else {
 #pragma unroll
-      for (int i = 0; i < 8; i++) o4[16 * i + 8 * rnd] = make_float4(g[i][0], g[i][1], g[i][2], g[i][3]);
+      for (int i = 0; i < 8; i++) o4[CH * i + 8 * rnd] = make_float4(g[i][0], g[i][1], g[i][2], g[i][3]);
     }
   }
 }
@@ -2592,24 +2595,24 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(GCOW_DMV_
 // Variable rate (1-D closed-form domain) with each stream's block index every 16 blocks (index_words entries apart):
 // the shape of k_decode1d_var_lean -- LANES chunks of 16 blocks per workgroup, the workgroup's span of each stream
 // staged in LDS in turn -- with the 16 blocks' 64 values accumulated in registers across the streams and stored once.
-template <uint32_t LANES>
+template <uint32_t LANES, uint32_t CH>
 __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params p, const uint64_t* __restrict__ in,
                                                              uint64_t stream_words, const uint64_t* __restrict__ index,
                                                              uint64_t index_words, uint64_t nchunks, uint32_t nstreams,
                                                              uint64_t cfirst)
 {
 #pragma clang fp contract(off)
-  constexpr uint32_t CAP = LANES * 16 * 80 / 64;
+  constexpr uint32_t CAP = LANES * CH * 80 / 64;
   __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
   __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
   const uint32_t tid = threadIdx.x;
   stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
   const uint64_t c0 = cfirst + (uint64_t)blockIdx.x * LANES;
   const uint64_t c = c0 + tid;
-  const uint64_t b0 = c * 16, b1 = min<uint64_t>(b0 + 16, F.nblocks);
-  float acc[16][4];
+  const uint64_t b0 = c * CH, b1 = min<uint64_t>(b0 + CH, F.nblocks);
+  float acc[CH][4];
 #pragma unroll
-  for (int k = 0; k < 16; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
+  for (int k = 0; k < (int)CH; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
   for (uint32_t r = 0; r < nstreams; r++) {
     const uint64_t* sr = in + (uint64_t)r * stream_words;
     const uint64_t* ix = index + (uint64_t)r * index_words;
@@ -2627,7 +2630,7 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
     uint64_t pos = ix[c];
     auto run = [&](const auto& win) {
 #pragma unroll
-      for (int k = 0; k < 16; k++) {
+      for (int k = 0; k < (int)CH; k++) {
         if (b0 + k < b1) {
           float f[4];
           decode_block1d_var(win, pos, dt7, p.minexp, p.maxprec, f);
@@ -2644,10 +2647,10 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
     }
   }
   if (c >= nchunks) return;
-  mean_scale<64>(&acc[0][0], nstreams);
+  mean_scale<CH * 4>(&acc[0][0], nstreams);
   float* out = (float*)F.data;
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
+  for (int k = 0; k < (int)CH; k++) {
     const uint64_t b = b0 + k;
     if (b < b1) {
       float v[4];
@@ -2665,12 +2668,12 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
 __global__ __launch_bounds__(256) void k_decode_mean1d_generic(FieldDesc F, Params p, const uint64_t* __restrict__ in,
                                                                uint64_t stream_words, const uint64_t* __restrict__ index,
                                                                uint64_t index_words, uint64_t nchunks,
-                                                               uint32_t nstreams)
+                                                               uint32_t nstreams, uint32_t chunk)
 {
 #pragma clang fp contract(off)
   const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (c >= nchunks) return;
-  const uint64_t b0 = c * 16, b1 = min<uint64_t>(b0 + 16, F.nblocks);
+  const uint64_t b0 = c * chunk, b1 = min<uint64_t>(b0 + chunk, F.nblocks);  // chunk <= 16
   float acc[16][4];
 #pragma unroll
   for (int k = 0; k < 16; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
@@ -3108,7 +3111,8 @@ hipError_t launch_stitch_shards(uint64_t* dst, uint64_t dst_words, const uint64_
 }
 
 hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t stream_words,
-                                uint32_t nstreams, const uint64_t* index, uint64_t index_words, void* stream)
+                                uint32_t nstreams, const uint64_t* index, uint64_t index_words, void* stream,
+                                uint32_t chunk)
 {
   if (!F.nblocks) return hipSuccess;
   hipStream_t st = S(stream);
@@ -3143,26 +3147,39 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
     }
     return hipGetLastError();
   }
-  const uint64_t nchunks = (F.nblocks + 15) / 16;
+  // variable rate: one lane per index chunk of `chunk` blocks (the streams' index stride, 8 or 16)
+  if (chunk != 8 && chunk != 16) return hipErrorInvalidValue;
+  const uint64_t nchunks = (F.nblocks + chunk - 1) / chunk;
   if (!(p.minbits <= 1 && p.maxbits >= 160)) {  // a budget can truncate blocks: generic decoder
     k_decode_mean1d_generic<<<(uint32_t)((nchunks + 255) / 256), 256, 0, st>>>(F, p, in, stream_words, index,
-                                                                              index_words, nchunks, nstreams);
+                                                                              index_words, nchunks, nstreams, chunk);
     return hipGetLastError();
   }
   // complete workgroups (128 whole chunks of full blocks, contiguous output) by the lean kernel, the rest by the
   // general one
   uint64_t nlean = 0;
   if (F.vec) {
-    const uint64_t fullchunks = (F.n[0] / 4) / 16;
+    const uint64_t fullchunks = (F.n[0] / 4) / chunk;
     nlean = std::min<uint64_t>(fullchunks, nchunks) / 128;
-    if (nlean)
-      k_decode_mean1d_var_lean<128, 64><<<(uint32_t)nlean, 128, 0, st>>>(F, p, in, stream_words, index, index_words,
-                                                                          nchunks, nstreams);
+    if (nlean) {
+      if (chunk == 8)
+        k_decode_mean1d_var_lean<128, 64, 8><<<(uint32_t)nlean, 128, 0, st>>>(F, p, in, stream_words, index,
+                                                                              index_words, nchunks, nstreams);
+      else
+        k_decode_mean1d_var_lean<128, 64, 16><<<(uint32_t)nlean, 128, 0, st>>>(F, p, in, stream_words, index,
+                                                                               index_words, nchunks, nstreams);
+    }
   }
   const uint64_t cfirst = nlean * 128;
-  if (cfirst < nchunks)
-    k_decode_mean1d_var<128><<<(uint32_t)((nchunks - cfirst + 127) / 128), 128, 0, st>>>(
-        F, p, in, stream_words, index, index_words, nchunks, nstreams, cfirst);
+  if (cfirst < nchunks) {
+    const uint32_t g = (uint32_t)((nchunks - cfirst + 127) / 128);
+    if (chunk == 8)
+      k_decode_mean1d_var<128, 8><<<g, 128, 0, st>>>(F, p, in, stream_words, index, index_words, nchunks, nstreams,
+                                                     cfirst);
+    else
+      k_decode_mean1d_var<128, 16><<<g, 128, 0, st>>>(F, p, in, stream_words, index, index_words, nchunks, nstreams,
+                                                      cfirst);
+  }
   return hipGetLastError();
 }
 

@@ -99,7 +99,8 @@ hipError_t launch_stitch_shards(uint64_t* dst, uint64_t dst_words, const uint64_
                                 const uint64_t* lens, uint32_t nshards, void* stream);
 // mean of nstreams 1-D streams (fixed rate: any params; variable: closed-form domain + index every 16 blocks)
 hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t stream_words,
-                                uint32_t nstreams, const uint64_t* index, uint64_t index_words, void* stream);
+                                uint32_t nstreams, const uint64_t* index, uint64_t index_words, void* stream,
+                                uint32_t chunk = 16);  // chunk: variable rate's index stride, 8 or 16
 hipError_t launch_stage(int which, int dims, const void* a, const void* b, uint32_t n, void* out, uint32_t x0,
                         uint32_t x1, void* out2, uint32_t slot_words, void* stream);
 hipError_t launch_fill_normal(float* out, uint64_t count, double sigma, uint64_t seed, int inject, void* stream);

@@ -272,7 +272,7 @@ gcow_status gcow_stitch_shards_device(uint64_t* d_dst, uint64_t dst_words, const
  * + 2 words (the decoders read 64-bit windows past a stream's last bit; GCOW_ERR_INVALID otherwise). Fixed rate: any
  * parameters, d_index NULL and index_words = index_stride = 0. Variable rate: any parameters (minbits <= 1,
  * maxbits >= 160 take the closed-form decoder, others the generic one) and every stream's block index (index_stride
- * 16, entries index_words apart at d_index, as gcow_encode_device writes them).
+ * 8 or 16, entries index_words apart at d_index, as gcow_encode_device writes them).
  */
 gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p, const uint64_t* d_streams,
                                     size_t streams_bytes, uint64_t stream_words, uint32_t nstreams,

@@ -101,12 +101,15 @@ def _mean_op(orc, mode):
 
 @pytest.mark.parametrize("mode", list(MEAN_MODES))
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_decode_mean_vs_oracle(gc, orc, mode, world):
+@pytest.mark.parametrize("stride", [16, 8])
+def test_decode_mean_vs_oracle(gc, orc, mode, world, stride):
     n = 4 * 20001 + 2  # a partial last block; > 128 index chunks
     op = _mean_op(orc, mode)
     fixed = op.minbits == op.maxbits
+    if fixed and stride != 16:
+        pytest.skip("fixed rate takes no index")
     buckets = [_bucket(orc, n, 900 + r, mode.startswith("bf16")) for r in range(world)]
-    encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else 16) for b in buckets]
+    encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else stride) for b in buckets]
     lens = [e.bits for e in encs]
     sw = max((b + 63) // 64 for b in lens) + (0 if fixed else 1)
     streams = torch.zeros(world * sw + 2, dtype=torch.int64, device="cuda")
@@ -116,7 +119,7 @@ def test_decode_mean_vs_oracle(gc, orc, mode, world):
     if not fixed:
         ni = encs[0].index.numel()
         idx = torch.cat([e.index[:ni] for e in encs])
-    got = gc.decode_mean(streams, sw, world, n, _P(gc, op), idx, ni, 0 if fixed else 16)
+    got = gc.decode_mean(streams, sw, world, n, _P(gc, op), idx, ni, 0 if fixed else stride)
     want = _oracle_mean(orc, [orc.compress(b, op)[0] for b in buckets], op, n)
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
@@ -131,15 +134,18 @@ def _bf16_rne(a: np.ndarray) -> np.ndarray:
 @pytest.mark.parametrize("mode", list(MEAN_MODES))
 @pytest.mark.parametrize("world", [1, 3])
 @pytest.mark.parametrize("layout", ["contiguous", "strided"])
-def test_decode_mean_bf16_output(gc, orc, mode, world, layout):
+@pytest.mark.parametrize("stride", [16, 8])
+def test_decode_mean_bf16_output(gc, orc, mode, world, layout, stride):
     """decode_mean into a bf16 bucket (the hook's receive side for bf16 gradients): the fp32 mean of the oracle
     decodes, rounded to nearest even, written in place -- contiguous (8-byte block stores, the lean kernels' transposed
     stores) and strided (value stores)."""
     n = 4 * 20001 + 2
     op = _mean_op(orc, mode)
     fixed = op.minbits == op.maxbits
+    if fixed and stride != 16:
+        pytest.skip("fixed rate takes no index")
     buckets = [_bucket(orc, n, 700 + r, mode.startswith("bf16")) for r in range(world)]
-    encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else 16) for b in buckets]
+    encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else stride) for b in buckets]
     sw = max((e.bits + 63) // 64 for e in encs) + (0 if fixed else 1)
     streams = torch.zeros(world * sw + 2, dtype=torch.int64, device="cuda")
     for r, e in enumerate(encs):
@@ -150,7 +156,7 @@ def test_decode_mean_bf16_output(gc, orc, mode, world, layout):
         idx = torch.cat([e.index[:ni] for e in encs])
     base = torch.full((2 * n,), -1.0, dtype=torch.bfloat16, device="cuda")
     out = base[:n] if layout == "contiguous" else base[::2]
-    got = gc.decode_mean(streams, sw, world, n, _P(gc, op), idx, ni, 0 if fixed else 16, out=out)
+    got = gc.decode_mean(streams, sw, world, n, _P(gc, op), idx, ni, 0 if fixed else stride, out=out)
     want = _bf16_rne(_oracle_mean(orc, [orc.compress(b, op)[0] for b in buckets], op, n))
     torch.cuda.synchronize()
     assert got.data_ptr() == out.data_ptr()
@@ -161,13 +167,14 @@ def test_decode_mean_bf16_output(gc, orc, mode, world, layout):
 
 @pytest.mark.parametrize("out_dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_decode_mean_stage_parts(gc, orc, world, out_dtype):
+@pytest.mark.parametrize("stride", [16, 8])
+def test_decode_mean_stage_parts(gc, orc, world, out_dtype, stride):
     """k_decode_mean1d_var_lean stages each stream's span of a workgroup (128 chunks of 16 blocks) in 1, 2 or 4 parts
     (a stage of 64 bits per block). Ranks hold data of very different magnitudes at accuracy 1e-6: N(0, 1e4) codes
     ~137 bits per block (every group in 4 parts), N(0, 1) ~100 (2 parts), N(0, 1e-3) ~64 (1 part, or 2); inside rank 0 the
     groups alternate between the first two. nchunks is a whole number of workgroups, so the last group's span runs to
     stream_words, far past the shorter ranks' streams. Bit-exact vs the oracle mean, fp32 and bf16 out."""
-    wg = 128 * 16 * 4  # values per workgroup
+    wg = 128 * stride * 4  # values per workgroup (128 chunks of `stride` blocks)
     n = wg * 7
     rng = np.random.default_rng(31337 + world)
     scales = [1e4, 1.0, 1e-3]
@@ -180,7 +187,7 @@ def test_decode_mean_stage_parts(gc, orc, world, out_dtype):
         buckets.append(a)
     op = orc.accuracy(1e-6)
     p = _P(gc, op)
-    encs = [gc.encode(_dev(b), p, index_stride=16) for b in buckets]
+    encs = [gc.encode(_dev(b), p, index_stride=stride) for b in buckets]
     lens = [e.bits for e in encs]
     bpb = [b / (n // 4) for b in lens]
     assert bpb[0] > 100 and (world < 2 or 80 < bpb[1] < 128) and (world < 3 or bpb[2] < 72), bpb
@@ -192,12 +199,12 @@ def test_decode_mean_stage_parts(gc, orc, world, out_dtype):
     idx = torch.cat([e.index[:ni] for e in encs])
     want = _oracle_mean(orc, [orc.compress(b, op)[0] for b in buckets], op, n)
     if out_dtype == "f32":
-        got = gc.decode_mean(streams, sw, world, n, p, idx, ni, 16)
+        got = gc.decode_mean(streams, sw, world, n, p, idx, ni, stride)
         torch.cuda.synchronize()
         assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
     else:
         out = torch.empty(n, dtype=torch.bfloat16, device="cuda")
-        gc.decode_mean(streams, sw, world, n, p, idx, ni, 16, out=out)
+        gc.decode_mean(streams, sw, world, n, p, idx, ni, stride, out=out)
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().view(torch.int16).numpy().view(np.uint16), _bf16_rne(want))
 

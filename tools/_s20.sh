@@ -1,0 +1,7 @@
+export GPU_SESSION_STRICT=1
+T="python -u -m pytest tests/test_gpu_exchange.py -m gpu -x -q --timeout 120 --timeout-method thread -k 'decode_mean'"
+tools/gpu_session.sh "300|t_dm|$T" \
+ "150|a16|python tools/dmean_stride_time.py --stride 16" \
+ "150|a8|python tools/dmean_stride_time.py --stride 8" \
+ "150|b16|python tools/dmean_stride_time.py --stride 16" \
+ "150|b8|python tools/dmean_stride_time.py --stride 8"
