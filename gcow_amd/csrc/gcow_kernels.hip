@@ -1460,6 +1460,28 @@ __host__ __device__ constexpr DecTabPG make_dec_pair_gather()
 
 __device__ const DecTabPG g_dec_pair_gather = make_dec_pair_gather();
 
+// The variable-rate lean decoder's LDS image: the pair table as 16-bit entries (n < 3, next 10 bits) -> nibbles
+// [0, 8), bits taken [8, 12), min(n, 3) after [12, 14), two planes taken [14] (dec_pair_cx's fields), then the plane
+// table's 640 entries (DecTab7) for a step that may take one plane only (the block's last coded plane, or the last
+// of the 8-plane group window) and for the general decoder. 7424 bytes.
+struct alignas(16) DecTabLP {
+  uint16_t v[3 * 1024 + 5 * 128];
+};
+
+__host__ __device__ constexpr DecTabLP make_dec_lean_pair()
+{
+  DecTabLP T{};
+  for (uint32_t t = 0; t < 3 * 1024; t++) {
+    const uint32_t e = dec_pair_cx(t);
+    T.v[t] = (uint16_t)((e & 255u) | (((e >> 12) & 15u) << 8) | (((e >> 18) & 3u) << 12) | (((e >> 20) & 1u) << 14));
+  }
+  const DecTab7 S = make_dec_tab7();
+  for (uint32_t t = 0; t < 5 * 128; t++) T.v[3 * 1024 + t] = S.v[t];
+  return T;
+}
+
+__device__ const DecTabLP g_dec_lean_pair = make_dec_lean_pair();
+
 
 __device__ __forceinline__ void window_to_coeffs_lds(const uint32_t* gt, uint64_t Y, int top, uint32_t* u)
 {
@@ -1847,8 +1869,10 @@ __device__ __forceinline__ uint64_t lds_win64(const uint32_t* w, uint32_t pos)
   return ((uint64_t)__builtin_amdgcn_alignbit(c, b, pos) << 32) | __builtin_amdgcn_alignbit(b, a, pos);
 }
 
-// returns false when the block needs the general decoder (pos unchanged then)
-__device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& pos, const uint16_t* dt7, int cexp,
+// returns false when the block needs the general decoder (pos unchanged then). PAIR: tab is the DecTabLP image and
+// the group phase decodes up to two planes per lookup; else tab is DecTab7.
+template <bool PAIR = false>
+__device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& pos, const uint16_t* tab, int cexp,
                                                  int maxprec, float* f)
 {
   const uint64_t w = lds_win64(sw, pos);
@@ -1871,17 +1895,46 @@ __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& p
   uint32_t off = 9u + (uint32_t)z, wbase = pos;
   uint32_t n = 0, G = 0;
   int j = 0;
-  while (n < 3 && j < nbelow && j < 8) {
-    if (off > 57u) {
-      wbase += off;
-      gw = lds_win64(sw, wbase);
-      off = 0;
+  if constexpr (PAIR) {
+    // (n, 10 bits) -> one or two planes; a second plane past the block's coded planes or past the 8-plane window is
+    // not taken: that step re-reads the plane table for the first plane alone
+    const uint16_t* dt7 = tab + 3 * 1024;
+    const int lim = min(nbelow, 8);
+    while (n < 3 && j < lim) {
+      if (off > 54u) {
+        wbase += off;
+        gw = lds_win64(sw, wbase);
+        off = 0;
+      }
+      const uint32_t b = (uint32_t)(gw >> off) & 1023u;
+      const uint32_t e = tab[(n << 10) | b];
+      uint32_t nib = e & 255u, len = (e >> 8) & 15u, nn = (e >> 12) & 3u, two = e >> 14;
+      if (two && j + 1 >= lim) {
+        const uint32_t e7 = dt7[(n << 7) | (b & 127u)];
+        nib = e7 & 15u;
+        len = (e7 >> 4) & 15u;
+        nn = e7 >> 8;
+        two = 0;
+      }
+      G |= nib << (4 * j);
+      off += len;
+      n = nn;
+      j += 1 + (int)two;
     }
-    const uint32_t e = dt7[(n << 7) | ((uint32_t)(gw >> off) & 127u)];
-    G |= (e & 15u) << (4 * j);
-    off += (e >> 4) & 15u;
-    n = e >> 8;
-    j++;
+  } else {
+    const uint16_t* dt7 = tab;
+    while (n < 3 && j < nbelow && j < 8) {
+      if (off > 57u) {
+        wbase += off;
+        gw = lds_win64(sw, wbase);
+        off = 0;
+      }
+      const uint32_t e = dt7[(n << 7) | ((uint32_t)(gw >> off) & 127u)];
+      G |= (e & 15u) << (4 * j);
+      off += (e >> 4) & 15u;
+      n = e >> 8;
+      j++;
+    }
   }
   if (n < 3 && j < nbelow) return false;  // group phase longer than 8 planes
   const uint32_t vpos = wbase + off;
@@ -1956,6 +2009,9 @@ __device__ __forceinline__ void xpose8_stage(float (&g)[8][4], uint32_t lane)
 #ifndef GCOW_VDEC_CAPB
 #define GCOW_VDEC_CAPB 64
 #endif
+#ifndef GCOW_VDEC_LPAIR
+#define GCOW_VDEC_LPAIR 0  // k_decode1d_var_lean's group phase through the pair table (7.4 KB more LDS per workgroup)
+#endif
 #ifndef GCOW_VDEC_BIGB
 #define GCOW_VDEC_BIGB 144
 #endif
@@ -1982,12 +2038,13 @@ __device__ __forceinline__ bool vdec_left_to_big(const FieldDesc& F, const uint6
 // One group: its span staged in sw (CAP words), each lane's 16 blocks decoded by the lean block decoder, stored
 // through the 8 x 8 lane transposes. BIG: the second pass (stage the caller's sw only after a barrier: the previous
 // group's readers are done); else the main kernel, which stages dt7 with the span in one round trip.
-template <uint32_t LANES, uint32_t CAP, bool BIG>
+template <uint32_t LANES, uint32_t CAP, bool BIG, bool LP = false>
 __device__ __forceinline__ void vdec_group(const FieldDesc& F, const Params& p, const uint64_t* __restrict__ in,
                                            uint64_t in_words, const uint64_t* __restrict__ index, uint64_t nchunks,
                                            uint64_t base_bits, uint64_t* __restrict__ end_out, uint64_t c0,
-                                           uint16_t* dt7, uint64_t* sw)
+                                           uint16_t* dtab, uint64_t* sw)
 {
+  uint16_t* dt7 = LP ? dtab + 3 * 1024 : dtab;  // LP: dtab holds the DecTabLP image
   const uint32_t tid = threadIdx.x;
   const uint64_t w0 = ((base_bits + index[c0]) >> 6) & ~1ull;  // 16-byte aligned start
   const uint64_t wend = c0 + LANES < nchunks ? ((base_bits + index[c0 + LANES] + 63) >> 6) : in_words;
@@ -1996,6 +2053,7 @@ __device__ __forceinline__ void vdec_group(const FieldDesc& F, const Params& p, 
   const uint64_t c = c0 + tid;
   const uint64_t mine = c < nchunks ? index[c] : 0ull;
   if constexpr (BIG) __syncthreads();
+  else if constexpr (LP) stage_lds16<LANES, sizeof(DecTabLP) / 16>(dtab, &g_dec_lean_pair, sizeof(DecTabLP));
   else stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
   if (staged) stage_lds16<LANES, (CAP + 4) / 2>(sw, in + w0, (uint32_t)(8 * span));
   __syncthreads();
@@ -2036,7 +2094,7 @@ __device__ __forceinline__ void vdec_group(const FieldDesc& F, const Params& p, 
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const uint32_t start = pos;
-      if (!dec_block1d_lean(sw32, pos, dt7, cexp, maxprec, g[k])) {
+      if (!dec_block1d_lean<LP>(sw32, pos, dtab, cexp, maxprec, g[k])) {
         uint64_t p64 = start;
         decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, g[k]);
         pos = (uint32_t)p64;
@@ -2064,14 +2122,15 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params
                                                              uint64_t* __restrict__ end_out, uint64_t* __restrict__ left,
                                                              uint64_t seq)
 {
-  __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
+  constexpr bool LP = GCOW_VDEC_LPAIR;
+  __shared__ __attribute__((aligned(16))) uint16_t dtab[LP ? 3 * 1024 + 5 * 128 : 5 * 128];
   __shared__ __attribute__((aligned(16))) uint64_t sw[vdec_cap<LANES>() + 4];
   const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
   if (vdec_left_to_big<LANES>(F, index, in_words, nchunks, base_bits, c0)) {  // workgroup-uniform
     if (left && threadIdx.x == 0) atomicMax((unsigned long long*)left, (unsigned long long)seq);  // second pass has work
     return;
   }
-  vdec_group<LANES, vdec_cap<LANES>(), false>(F, p, in, in_words, index, nchunks, base_bits, end_out, c0, dt7, sw);
+  vdec_group<LANES, vdec_cap<LANES>(), false, LP>(F, p, in, in_words, index, nchunks, base_bits, end_out, c0, dtab, sw);
 }
 
 template <uint32_t LANES>
@@ -2502,6 +2561,9 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
 #ifndef GCOW_DMV8_WAVES
 #define GCOW_DMV8_WAVES 5  // 8-block chunks: 32 sums per lane, 96 VGPRs (2 spilled) at 5 waves: 3.43 -> 3.05 ms (W = 8)
 #endif
+#ifndef GCOW_DMV_LPAIR
+#define GCOW_DMV_LPAIR 1  // the lean block decoder's group phase through the 16-bit pair table (DecTabLP)
+#endif
 // Variable rate (1-D closed-form domain), the lean decoder's shape (k_decode1d_var_lean): LANES 16-block chunks per
 // workgroup; for each stream in rank order its span is staged in LDS (in 1, 2 or 4 parts, as there) and each lane
 // decodes its chunk into 64 registers of sums; the means leave through the 8 x 8 lane transposes as whole-line
@@ -2518,14 +2580,17 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(CH == 8 ?
 #pragma clang fp contract(off)
   constexpr uint32_t CAP = LANES * CH * CAPB / 64;
   static_assert(LANES % 32 == 0 && CAP >= 32 * CH * 140 / 64 + 4 && CH % 8 == 0, "a quarter workgroup's longest span must fit");
-  __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
+  constexpr bool LP = GCOW_DMV_LPAIR && CH == 8;  // CH = 16: the 7.4 KB image would cost a wave per SIMD (LDS)
+  __shared__ __attribute__((aligned(16))) uint16_t dtab[LP ? 3 * 1024 + 5 * 128 : 5 * 128];
+  const uint16_t* dt7 = LP ? dtab + 3 * 1024 : dtab;
   __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
   const uint32_t tid = threadIdx.x;
   const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
   const uint64_t c = c0 + tid;
   const uint32_t* sw32 = (const uint32_t*)sw;
   const int cexp = 4 - p.minexp, maxprec = (int)min(p.maxprec, 64u);
-  stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
+  if constexpr (LP) stage_lds16<LANES, sizeof(DecTabLP) / 16>(dtab, &g_dec_lean_pair, sizeof(DecTabLP));
+  else stage_lds16<LANES, sizeof(DecTab7) / 16>(dtab, &g_dec_tab7, sizeof(DecTab7));
   float acc[CH][4];
 #pragma unroll
   for (int k = 0; k < (int)CH; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
@@ -2556,7 +2621,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(CH == 8 ?
       for (int k = 0; k < (int)CH; k++) {
         const uint32_t start = pos;
         float f[4];
-        if (!dec_block1d_lean(sw32, pos, dt7, cexp, maxprec, f)) {
+        if (!dec_block1d_lean<LP>(sw32, pos, dtab, cexp, maxprec, f)) {
           uint64_t p64 = start;
           decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, f);
           pos = (uint32_t)p64;
