@@ -588,8 +588,9 @@ def leg_configs(ctx):
         er["traffic"], src = load_pmc_traffic("k_count1d_var_tile", name + "_256Mi")
         er["traffic_source"] = src
         # the receive side (the caller's codec cost is compress + decompress, hw/models/train_imagenet.py:458-467):
-        # the 1-D variable-rate decode of this stream (block index every 16 blocks) into fp32
-        e = enc(xb, st)
+        # the 1-D variable-rate decode of this stream (block index every 16 blocks) into fp32, given the stream as a
+        # receiver holds it (its own length, not the encoder's capacity-sized buffer)
+        e = exact_stream(enc(xb, st))
         back = torch.empty(n, dtype=torch.float32, device=ctx.dev)
         _, dper = timed(ctx, lambda: codec.decode(e, out=back, stream=st), 5, 20, stream=st)
         dk = sum(dper) / len(dper)
@@ -621,7 +622,7 @@ def leg_configs(ctx):
     st = torch.cuda.current_stream(ctx.dev)
     _, per = timed(ctx, lambda: enc(x32, st), 5, 20, stream=st)
     k_ms = sum(per) / len(per)
-    e = enc(x32, st)
+    e = exact_stream(enc(x32, st))
     cbits = e.bits
     back = torch.empty_like(x32)
     _, dper = timed(ctx, lambda: codec.decode(e, out=back, stream=st), 5, 20, stream=st)
@@ -636,6 +637,13 @@ def leg_configs(ctx):
     torch.cuda.empty_cache()
     out["decode_mean_w8"] = leg_decode_mean(ctx)
     return out
+
+
+def exact_stream(e):
+    """The Encoded `e` with its words cut to the stream's own length (the buffer a receiver holds): the variable-rate
+    decoder sizes its stage by the buffer's average bits per block (gcow_kernels.hip launch_decode1d_var)."""
+    from gcow_amd import codec
+    return codec.Encoded(e.stream(), e.bits_dev, e.shape, e.params, e.index, e.index_stride)
 
 
 def leg_decode_mean(ctx, W: int = 8):

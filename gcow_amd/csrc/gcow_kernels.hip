@@ -2009,6 +2009,9 @@ __device__ __forceinline__ void xpose8_stage(float (&g)[8][4], uint32_t lane)
 #ifndef GCOW_VDEC_CAPB
 #define GCOW_VDEC_CAPB 64
 #endif
+#ifndef GCOW_VDEC_ADAPT
+#define GCOW_VDEC_ADAPT 1  // launch_decode1d_var sizes the main kernel's stage by the stream buffer's average bits
+#endif
 #ifndef GCOW_VDEC_LPAIR
 #define GCOW_VDEC_LPAIR 0  // k_decode1d_var_lean's group phase through the pair table (7.4 KB more LDS per workgroup)
 #endif
@@ -2017,14 +2020,14 @@ __device__ __forceinline__ void xpose8_stage(float (&g)[8][4], uint32_t lane)
 #endif
 // Stage capacity in stream words: the main kernel's (GCOW_VDEC_CAPB bits per block on average) and the second pass's
 // (any span: a 1-D block codes at most 140 bits, plus the 16-byte alignment of the span's start)
-template <uint32_t LANES> constexpr uint32_t vdec_cap() { return LANES * 16 * GCOW_VDEC_CAPB / 64; }
+template <uint32_t LANES, uint32_t CAPB = GCOW_VDEC_CAPB> constexpr uint32_t vdec_cap() { return LANES * 16 * CAPB / 64; }
 template <uint32_t LANES> constexpr uint32_t vdec_cap_big() { return LANES * 16 * GCOW_VDEC_BIGB / 64; }
 
 // A group of LANES index chunks (one workgroup's work) whose span does not fit the main kernel's stage, and which is
 // whole (no partial chunk or block) with a contiguous output: left by the main kernel to k_decode1d_var_lean_big.
 // Not the last group: its span ends at the stream's end, which the index does not give (the buffer's end bounds it),
 // so it takes the main kernel's general path.
-template <uint32_t LANES>
+template <uint32_t LANES, uint32_t CAPB>
 __device__ __forceinline__ bool vdec_left_to_big(const FieldDesc& F, const uint64_t* index, uint64_t in_words,
                                                  uint64_t nchunks, uint64_t base_bits, uint64_t c0)
 {
@@ -2032,7 +2035,7 @@ __device__ __forceinline__ bool vdec_left_to_big(const FieldDesc& F, const uint6
   if (!whole || !F.vec) return false;
   const uint64_t w0 = ((base_bits + index[c0]) >> 6) & ~1ull;
   const uint64_t wend = (base_bits + index[c0 + LANES] + 63) >> 6;
-  return min<uint64_t>(wend, in_words) - w0 > vdec_cap<LANES>();
+  return min<uint64_t>(wend, in_words) - w0 > vdec_cap<LANES, CAPB>();
 }
 
 // One group: its span staged in sw (CAP words), each lane's 16 blocks decoded by the lean block decoder, stored
@@ -2115,7 +2118,7 @@ __device__ __forceinline__ void vdec_group(const FieldDesc& F, const Params& p, 
   if (end_out && c == nchunks - 1) *end_out = pos + 64 * w0;
 }
 
-template <uint32_t LANES>
+template <uint32_t LANES, uint32_t CAPB>
 __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params p, const uint64_t* __restrict__ in,
                                                              uint64_t in_words, const uint64_t* __restrict__ index,
                                                              uint64_t nchunks, uint64_t base_bits,
@@ -2124,13 +2127,13 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params
 {
   constexpr bool LP = GCOW_VDEC_LPAIR;
   __shared__ __attribute__((aligned(16))) uint16_t dtab[LP ? 3 * 1024 + 5 * 128 : 5 * 128];
-  __shared__ __attribute__((aligned(16))) uint64_t sw[vdec_cap<LANES>() + 4];
+  __shared__ __attribute__((aligned(16))) uint64_t sw[vdec_cap<LANES, CAPB>() + 4];
   const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
-  if (vdec_left_to_big<LANES>(F, index, in_words, nchunks, base_bits, c0)) {  // workgroup-uniform
+  if (vdec_left_to_big<LANES, CAPB>(F, index, in_words, nchunks, base_bits, c0)) {  // workgroup-uniform
     if (left && threadIdx.x == 0) atomicMax((unsigned long long*)left, (unsigned long long)seq);  // second pass has work
     return;
   }
-  vdec_group<LANES, vdec_cap<LANES>(), false, LP>(F, p, in, in_words, index, nchunks, base_bits, end_out, c0, dtab, sw);
+  vdec_group<LANES, vdec_cap<LANES, CAPB>(), false, LP>(F, p, in, in_words, index, nchunks, base_bits, end_out, c0, dtab, sw);
 }
 
 template <uint32_t LANES>
@@ -2142,7 +2145,7 @@ __device__ __forceinline__ void vdec_group_big(const FieldDesc& F, const Params&
   vdec_group<LANES, vdec_cap_big<LANES>(), true>(F, p, in, in_words, index, nchunks, base_bits, end_out, c0, dt7, sw);
 }
 
-template <uint32_t LANES>
+template <uint32_t LANES, uint32_t CAPB>
 __global__ __launch_bounds__(LANES) void k_decode1d_var_lean_big(FieldDesc F, Params p, const uint64_t* __restrict__ in,
                                                                  uint64_t in_words, const uint64_t* __restrict__ index,
                                                                  uint64_t nchunks, uint64_t base_bits,
@@ -2163,7 +2166,7 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean_big(FieldDesc F, Pa
     if (threadIdx.x == 0) ntodo = 0;
     __syncthreads();
     const uint64_t g = gb + (uint64_t)threadIdx.x * G + blockIdx.x;
-    if (g < ng && vdec_left_to_big<LANES>(F, index, in_words, nchunks, base_bits, g * LANES))
+    if (g < ng && vdec_left_to_big<LANES, CAPB>(F, index, in_words, nchunks, base_bits, g * LANES))
       todo[atomicAdd(&ntodo, 1u)] = threadIdx.x;
     __syncthreads();
     const uint32_t nt = ntodo;
@@ -3090,10 +3093,27 @@ hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64
     hipStream_t st = S(stream);
     uint64_t* left = vdec_flag_ring();
     if (left) left += seq % kVdecFlagRing;
-    k_decode1d_var_lean<L><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left,
-                                                       seq);
+    // the main kernel's stage: the smallest of 32 / 48 / 64 bits per block that holds 1.25 x the buffer's average
+    // (LDS sets its occupancy: 8 / 6 / 4.5 waves per SIMD; accuracy 1e-3 bf16, 24 bits per block: 0.43 -> 0.35 ms).
+    // The buffer is the caller's: a capacity-sized one (Encoder.words) reads as dense and keeps 64.
+    const uint64_t nb = F.nblocks ? F.nblocks : 1, avail = in_words * 64 - std::min<uint64_t>(base_bits, in_words * 64);
     const uint32_t gbig = (uint32_t)std::min<uint64_t>(ng, 1024);
-    k_decode1d_var_lean_big<L><<<gbig, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left, seq);
+    if (GCOW_VDEC_ADAPT && avail * 5 <= nb * 32 * 4) {
+      k_decode1d_var_lean<L, 32><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out,
+                                                             left, seq);
+      k_decode1d_var_lean_big<L, 32><<<gbig, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left,
+                                                         seq);
+    } else if (GCOW_VDEC_ADAPT && avail * 5 <= nb * 48 * 4) {
+      k_decode1d_var_lean<L, 48><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out,
+                                                             left, seq);
+      k_decode1d_var_lean_big<L, 48><<<gbig, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left,
+                                                         seq);
+    } else {
+      k_decode1d_var_lean<L, GCOW_VDEC_CAPB><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits,
+                                                                         end_out, left, seq);
+      k_decode1d_var_lean_big<L, GCOW_VDEC_CAPB><<<gbig, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits,
+                                                                     end_out, left, seq);
+    }
     return hipGetLastError();
   }
   k_decode1d_var<<<(uint32_t)((nchunks + 255) / 256), 256, 0, S(stream)>>>(F, p, in, index, chunk, nchunks, base_bits,

@@ -164,6 +164,27 @@ def test_var1d_decode_past_the_stage(gc, orc, tol, out_dtype):
         assert np.array_equal(got.cpu().view(torch.int16).numpy().view(np.uint16), _bf16_rne(ref))
 
 
+@pytest.mark.parametrize("tol,mix", [(1e-2, False), (1e-3, False), (1e-3, True), (3e-4, False), (1e-4, False),
+                                     (1e-4, True), (1e-6, True)])
+def test_var1d_decode_exact_stream_buffer(gc, orc, tol, mix):
+    """The lean variable-rate decoder given the stream in a buffer of its own size (e.stream(), not the encoder's
+    capacity-sized one): launch_decode1d_var then sizes the main kernel's stage by the average bits per block (32, 48
+    or 64), and groups past it take the second pass (mix: a quiet half and a loud half, so the average picks a small
+    stage that the loud groups overflow). Bit for bit against the oracle, whole and partial groups."""
+    n = 4 * 16 * 128 * 9 + 4 * 16 * 37 + 4 * 5 + 2
+    a = orc.gen_normal(n, 1e-3, 0xE5AC7 + int(-np.log10(tol)), True)
+    if mix:
+        a[: n // 2] *= np.float32(1e-3)
+        a[n // 2 + n // 8: n // 2 + n // 4] *= np.float32(30.0)
+    op = orc.accuracy(tol)
+    e, _ = dev_encode_bytes(gc, a, P(gc, op), 16)
+    ref = orc.decompress(orc.compress(a, op)[0], a.shape, op)
+    words = e.stream()
+    got = gc.decode(words, e.shape, e.params, e.index, e.index_stride)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), ref.view(np.uint32)), e.bits / ((n + 3) // 4)
+
+
 def test_decode_bf16_output_needs_1d(gc, orc):
     a = orc.gen_normal(16 * 16, 1e-3, 5, False).reshape(16, 16)
     e, _ = dev_encode_bytes(gc, a, gc.rate(16, 2))
