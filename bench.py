@@ -682,6 +682,11 @@ def leg_decode_mean(ctx, W: int = 8):
         _, per = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ix, ni, stride, out=mean, stream=st), 3, 10,
                        stream=st)
         k = sum(per) / len(per)
+        k8 = None
+        if stride:  # the same decode with the sharded hook's index spacing (8-block chunks)
+            _, per8 = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ix8, ni8, sstride, out=mean, stream=st), 3,
+                            10, stream=st)
+            k8 = round(sum(per8) / len(per8), 4)
         kname = "k_decode_mean_fixed1d<64>" if stride == 0 else "k_decode_mean1d_var<128>"
         # the sharded receive (ddp.compressed_sharded_hook): one rank's decode-mean of its 1/W shard from the W pieces
         # the all-to-all delivers (cut here from the same streams; the exchange itself is an N > 1 leg)
@@ -692,6 +697,7 @@ def leg_decode_mean(ctx, W: int = 8):
         ks = sum(sper) / len(sper)
         res[name] = {"streams": W, "values": n, "kernel_ms": round(k, 4), "bits_per_value": round(bits / W / n, 3),
                      "roofline": roof(bits / 8, n * 4, k, kname, basis="write"),
+                     "kernel_ms_index_stride8": k8,
                      "sharded_receive_kernel_ms": round(ks, 4), "sharded_receive_values": hi - lo,
                      "index_stride": stride, "sharded_index_stride": sstride}
         del buf, ix, ix8, pieces, pidx

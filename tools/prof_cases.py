@@ -62,24 +62,27 @@ def c5(reps):
 
 
 def vdec(reps):
-    """1-D variable-rate decode (accuracy 1e-6, block index every 16 blocks) of the fp32 and the bf16 C5 bucket."""
+    """1-D variable-rate decode (block index every 16 blocks) of the fp32 and the bf16 C5 bucket at accuracy 1e-6, and
+    of the bf16 one at 1e-3, each stream in a buffer of its own length (the stage is sized by its average)."""
     n = 256 << 20
     x = torch.empty(n, dtype=torch.float32, device="cuda")
     codec.fill_normal(x)
     out = torch.empty_like(x)
-    for src in (x, x.to(torch.bfloat16)):
-        e = codec.encode(src, codec.accuracy(1e-6), index_stride=16)
+    for src, tol in ((x, 1e-6), (x.to(torch.bfloat16), 1e-6), (x.to(torch.bfloat16), 1e-3)):
+        e = codec.encode(src, codec.accuracy(tol), index_stride=16)
+        e = codec.Encoded(e.stream(), e.bits_dev, e.shape, e.params, e.index, e.index_stride)
         for _ in range(reps):
             codec.decode(e, out=out)
         torch.cuda.synchronize()
 
 
 def dmean(reps, W=8):
-    """decode_mean over W streams of 256 Mi values: rate 16, then accuracy 1e-6."""
+    """decode_mean over W streams of 256 Mi values: rate 16, then accuracy 1e-6 with the block index every 16 and
+    every 8 blocks (the all-gather and the sharded hook's spacing)."""
     n = 256 << 20
     x = torch.empty(n, dtype=torch.float32, device="cuda")
     out = torch.empty_like(x)
-    for p, stride in ((codec.rate(16, 1), 0), (codec.accuracy(1e-6), 16)):
+    for p, stride in ((codec.rate(16, 1), 0), (codec.accuracy(1e-6), 16), (codec.accuracy(1e-6), 8)):
         enc = codec.Encoder((n,), torch.float32, p, index_stride=stride)
         ss, ix = [], []
         for r in range(W):
