@@ -241,6 +241,9 @@ gcow_status gcow_encode_device_append(const zfp_input* field, const gcow_params*
  * nearest even, torch's conversion) with libzfp 0.5.5 semantics. Fixed-rate streams
  * (minbits == maxbits) decode one block per thread; variable-rate streams need the index written by
  * gcow_encode_device (d_index/index_stride), or, with d_index == NULL, are decoded by a single sequential GPU lane.
+ * in_bytes may be the buffer's capacity; given the stream's own length (ceil(bits / 64) words), the 1-D
+ * variable-rate decoder sizes its LDS stage from the stream's average bits per block (more waves for compressible
+ * streams; the result is the same either way).
  */
 gcow_status gcow_decode_device(const zfp_input* field, const gcow_params* p, const void* d_in, size_t in_bytes,
                                const uint64_t* d_index, uint32_t index_stride, void* hip_stream);
