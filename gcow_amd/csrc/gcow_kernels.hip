@@ -2564,6 +2564,9 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
 #ifndef GCOW_DMV8_WAVES
 #define GCOW_DMV8_WAVES 5  // 8-block chunks: 32 sums per lane, 96 VGPRs (2 spilled) at 5 waves: 3.43 -> 3.05 ms (W = 8)
 #endif
+#ifndef GCOW_DMV8_SCALE
+#define GCOW_DMV8_SCALE 1  // 8-block chunks: the mean through mean_scale (a power-of-two world: the exact reciprocal)
+#endif
 #ifndef GCOW_DMV_LPAIR
 #define GCOW_DMV_LPAIR 1  // the lean block decoder's group phase through the 16-bit pair table (DecTabLP)
 #endif
@@ -2634,7 +2637,9 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(CH == 8 ?
       }
     }
   }
-  const float nf = (float)nstreams;  // a plain division here: the two-path mean_scale costs this kernel registers (+4 %)
+  // CH = 16: a plain division (the two-path mean_scale costs that kernel registers, +4 %)
+  if constexpr (CH == 8 && GCOW_DMV8_SCALE) mean_scale<CH * 4>(&acc[0][0], nstreams);
+  const float nf = CH == 8 && GCOW_DMV8_SCALE ? 1.0f : (float)nstreams;
   const uint32_t lane = tid & 63u, m = lane & 7u;
   float4* o4 = (float4*)F.data + (c - m) * CH + m;
   uint2* o2 = (uint2*)F.data + (c - m) * CH + m;  // bf16 output: 8 bytes per block, a chunk is one 128-byte line
