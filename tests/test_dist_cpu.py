@@ -385,7 +385,7 @@ def test_device_codec_cache_evicts_idle_only(monkeypatch):
     assert len(c._enc) == B
 
 
-def _sharded_exchange_worker(rank, world, port, q, mode, nvals, bf16):
+def _sharded_exchange_worker(rank, world, port, q, mode, nvals, bf16, stride=16):
     _init(rank, world, port)
     try:
         from gcow_amd import codec
@@ -404,16 +404,16 @@ def _sharded_exchange_worker(rank, world, port, q, mode, nvals, bf16):
         mine = torch.from_numpy(grads[rank].copy())
         x = mine.view(torch.bfloat16) if bf16 else mine
         fixed = codec.is_fixed(p)
-        words, bits, index = cdc.encode(x, p, 0 if fixed else 16)
+        words, bits, index = cdc.encode(x, p, 0 if fixed else stride)
         if fixed:
             pieces, pw, lo, hi = gdist.shard_pieces_fixed(words, nvals, p.maxbits)
             pidx, iw = None, 0
         else:
-            pieces, pw, pidx, iw, lo, hi = gdist.shard_pieces_variable(words, bits, index, nvals, 16)
+            pieces, pw, pidx, iw, lo, hi = gdist.shard_pieces_variable(words, bits, index, nvals, stride)
         flat = torch.full((nvals,), -7.0, dtype=torch.float32)
         shard = flat[lo:hi]
         if hi > lo:
-            cdc.decode_mean(pieces, pw, world, hi - lo, p, pidx, iw, 0 if fixed else 16, out=shard)
+            cdc.decode_mean(pieces, pw, world, hi - lo, p, pidx, iw, 0 if fixed else stride, out=shard)
         gdist.allgather_shards(flat, shard, nvals)
         acc = np.zeros(nvals, np.float32)
         for a in grads:
@@ -437,3 +437,11 @@ def test_sharded_pieces_gloo(world, mode, nvals, bf16):
     shards all-gathered -- equal, bit for bit, to the mean of the oracle decodes of the whole streams. Ragged last
     shards, partial last blocks, bf16 buckets, and buckets too small for every rank to own a shard (empty shards)."""
     _run(_sharded_exchange_worker, world, mode, nvals, bf16)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("mode,nvals,bf16", [("acc1e-6", 4 * 3000 + 3, False), ("acc1e-3", 4 * 2999, True)])
+def test_sharded_pieces_index8_gloo(world, mode, nvals, bf16):
+    """The same exchange with the block index every 8 blocks (the sharded hook's spacing, ddp.SHARDED_INDEX_STRIDE):
+    pieces cut and index slices rebased at 8-block granularity, bit for bit against the oracle mean."""
+    _run(_sharded_exchange_worker, world, mode, nvals, bf16, 8)
