@@ -2559,13 +2559,16 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
 }
 
 #ifndef GCOW_DMV_WAVES
-#define GCOW_DMV_WAVES 4
+#define GCOW_DMV_WAVES 3  // 16-block chunks: 64 sums per lane, no spills at 3 waves (4 waves: 33 spilled VGPRs)
 #endif
 #ifndef GCOW_DMV8_WAVES
 #define GCOW_DMV8_WAVES 5  // 8-block chunks: 32 sums per lane, 96 VGPRs (2 spilled) at 5 waves: 3.43 -> 3.05 ms (W = 8)
 #endif
 #ifndef GCOW_DMV8_SCALE
 #define GCOW_DMV8_SCALE 1  // 8-block chunks: the mean through mean_scale (a power-of-two world: the exact reciprocal)
+#endif
+#ifndef GCOW_DMV16_LPAIR
+#define GCOW_DMV16_LPAIR 1  // 16-block chunks too, at 3 waves (LDS): 3.67 -> 3.59 ms (profiles/r05_dmean16_lp_w3_ab.log)
 #endif
 #ifndef GCOW_DMV_LPAIR
 #define GCOW_DMV_LPAIR 1  // the lean block decoder's group phase through the 16-bit pair table (DecTabLP)
@@ -2586,7 +2589,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(CH == 8 ?
 #pragma clang fp contract(off)
   constexpr uint32_t CAP = LANES * CH * CAPB / 64;
   static_assert(LANES % 32 == 0 && CAP >= 32 * CH * 140 / 64 + 4 && CH % 8 == 0, "a quarter workgroup's longest span must fit");
-  constexpr bool LP = GCOW_DMV_LPAIR && CH == 8;  // CH = 16: the 7.4 KB image would cost a wave per SIMD (LDS)
+  constexpr bool LP = GCOW_DMV_LPAIR && (CH == 8 || GCOW_DMV16_LPAIR);
   __shared__ __attribute__((aligned(16))) uint16_t dtab[LP ? 3 * 1024 + 5 * 128 : 5 * 128];
   const uint16_t* dt7 = LP ? dtab + 3 * 1024 : dtab;
   __shared__ __attribute__((aligned(16))) uint64_t sw[CAP + 4];
