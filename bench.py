@@ -99,17 +99,15 @@ class Ctx:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.stub = args.stub
         self.group = self.world > 1 or (args.multi_legs and not args.stub)
-        if self.world == 1 and self.group:
-            os.environ.setdefault("MASTER_PORT", str(_free_port()))
-            os.environ.setdefault("RANK", "0")
-            os.environ.setdefault("WORLD_SIZE", "1")
+        # one rank (--multi-legs at N = 1): an in-process store, no port to race other jobs on the box for
+        solo = {"store": dist.HashStore(), "rank": 0, "world_size": 1} if self.world == 1 and self.group else {}
         if self.group:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if self.stub:
-                dist.init_process_group("gloo")
+                dist.init_process_group("gloo", **solo)
             else:
                 torch.cuda.set_device(self.local)
-                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local), **solo)
         self.dev = torch.device("cpu") if self.stub else torch.device("cuda", self.local)
         if not self.stub:
             torch.cuda.set_device(self.dev)

@@ -10,6 +10,7 @@
 """
 import os
 import socket
+import tempfile
 import sys
 
 import numpy as np
@@ -311,7 +312,7 @@ def _mp_worker(rank, world, port, q, what, mode):
     for p in (ROOT, os.path.join(ROOT, "tests")):
         if p not in sys.path:
             sys.path.insert(0, p)
-    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)  # a file:// rendezvous
     try:
         from gcow_amd import codec, ddp
         from gcow_amd import dist as gdist
@@ -366,13 +367,14 @@ def test_exchange_multiprocess_device_codec(gc, what, mode, world):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_mp_worker, args=(r, world, port, q, what, mode)) for r in range(world)]
-    for pr in procs:
-        pr.start()
-    res = [q.get(timeout=100) for _ in procs]
-    for pr in procs:
-        pr.join(timeout=60)
+    with tempfile.TemporaryDirectory() as d:  # a file rendezvous: no port to race other jobs on the box for
+        init = "file://" + os.path.join(d, "rdv")
+        procs = [ctx.Process(target=_mp_worker, args=(r, world, init, q, what, mode)) for r in range(world)]
+        for pr in procs:
+            pr.start()
+        res = [q.get(timeout=100) for _ in procs]
+        for pr in procs:
+            pr.join(timeout=60)
     assert all(ok is True for _, ok in res), res
 
 
@@ -380,12 +382,9 @@ def test_exchange_multiprocess_device_codec(gc, what, mode, world):
 @pytest.fixture
 def nccl_world1():
     import torch.distributed as dist
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
-                            device_id=torch.device("cuda", 0))
+    # an in-process store: no port to race another job on the box for (a free port picked, closed and bound again
+    # was once taken in between: EADDRINUSE)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=torch.device("cuda", 0))
     yield
     dist.destroy_process_group()
 
