@@ -1,4 +1,4 @@
-# round-end set: full GPU tests, smoke, C2/C5 measurement + bench (measure_round), decoder measurement (measure_dec)
+# round-end set, part 1: full GPU tests, smoke, C2/C5 measurement + bench (measure_round)
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -7,5 +7,4 @@ tail -3 gpurun_out/r05_pytest_gpu_final.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r05_smoke_final.log 2>&1
 tail -1 gpurun_out/r05_smoke_final.log
 tools/measure_round.sh r05c
-tools/measure_dec.sh r05c
-echo all done
+echo part1 done
