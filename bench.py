@@ -30,7 +30,6 @@ import argparse
 import json
 import os
 import platform
-import socket
 import statistics
 import subprocess
 import sys
@@ -70,20 +69,18 @@ def parse(argv=None):
 
 
 # ------------------------------------------------------------------------------------------------------ launcher
-def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def launcher_cmd(nproc: int, argv) -> list:
+    """torchrun's single-node standalone rendezvous on 127.0.0.1: its c10d store binds port 0 itself and the workers
+    are handed the port it got (no port picked here and released before torchrun binds it: VERDICT r5's race)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr=127.0.0.1",
+            "--nproc-per-node=%d" % nproc, os.path.abspath(__file__)] + list(argv)
 
 
 def launch(args, argv) -> int:
     """N > 1 without a torchrun environment: start N ranks (one process per GPU) through torchrun on 127.0.0.1, each
     with the argument list this process was given (`argv`), and return its exit code. Called before anything
     initialises HIP in this process."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
-           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + list(argv)
+    cmd = launcher_cmd(args.gpus, argv)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env["GCOW_BENCH_LAUNCHER"] = "self"
@@ -895,7 +892,8 @@ def stub_worker(ctx: Ctx):
     t = torch.ones(1 << 12)
     wall, _ = timed(ctx, lambda: t.sum(), ctx.args.warmup, ctx.args.steps)
     wall = ctx.max_over_ranks([wall])[0]
-    me = [ctx.rank, ctx.local, ctx.world, os.environ.get("GCOW_BENCH_LAUNCHER", "torchrun")]
+    me = [ctx.rank, ctx.local, ctx.world, os.environ.get("GCOW_BENCH_LAUNCHER", "torchrun"),
+          os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")]
     ranks = [None] * ctx.world
     if ctx.world > 1:
         dist.all_gather_object(ranks, me)

@@ -3056,8 +3056,11 @@ hipError_t launch_scan_blocks(const uint32_t* lens, uint32_t nblocks, uint64_t* 
 
 // The second-pass flag words of launch_decode1d_var: kVdecFlagRing zeroed uint64 words per device, allocated on first
 // use and kept for the life of the process (nullptr if the allocation fails: the second pass then checks every group).
+// The first use allocates and zeroes on the caller's stream and waits for it; a first use inside stream capture
+// (where neither is allowed) returns nullptr instead -- that decode checks every group, and the ring is allocated by
+// the next uncaptured call.
 constexpr uint32_t kVdecFlagRing = 256;
-static uint64_t* vdec_flag_ring()
+static uint64_t* vdec_flag_ring(hipStream_t st)
 {
   static std::mutex mu;
   static uint64_t* ring[64] = {};
@@ -3068,12 +3071,18 @@ static uint64_t* vdec_flag_ring()
   }
   std::lock_guard<std::mutex> lk(mu);
   if (!ring[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
     uint64_t* r = nullptr;
     if (hipMalloc((void**)&r, kVdecFlagRing * sizeof(uint64_t)) != hipSuccess) {
       (void)hipGetLastError();
       return nullptr;
     }
-    if (hipMemset(r, 0, kVdecFlagRing * sizeof(uint64_t)) != hipSuccess) {
+    if (hipMemsetAsync(r, 0, kVdecFlagRing * sizeof(uint64_t), st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
       (void)hipGetLastError();
       (void)hipFree(r);
       return nullptr;
@@ -3099,7 +3108,7 @@ hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64
     static std::atomic<uint64_t> g_seq{1};
     const uint64_t seq = g_seq.fetch_add(1);
     hipStream_t st = S(stream);
-    uint64_t* left = vdec_flag_ring();
+    uint64_t* left = vdec_flag_ring(st);
     if (left) left += seq % kVdecFlagRing;
     // the main kernel's stage: the smallest of 32 / 48 / 64 bits per block that holds 1.25 x the buffer's average
     // (LDS sets its occupancy: 8 / 6 / 4.5 waves per SIMD; accuracy 1e-3 bf16, 24 bits per block: 0.43 -> 0.35 ms).

@@ -12,8 +12,9 @@ PCIe copies per step. Two device-resident replacements:
   (gcow_decode_mean_device: acc = 0 + x_0 + x_1 + ... in rank order, then / world). At rate r the wire carries r/32
   of the fp32 bytes per rank.
 
-Both register with `ddp_model.register_comm_hook(make_hook_state(...), hook)` (variable rate: the state's exchange
-group is created by `GcowHookState.setup()`, a collective every rank calls at the same point). `GcowHookState.codec` defaults to the
+All register with `ddp_model.register_comm_hook(make_hook_state(hook=hook, ...), hook)` (variable rate and the sharded
+hook: the state's exchange group is created by `GcowHookState.setup()`, a collective every rank calls at the same
+point). `GcowHookState.codec` defaults to the
 device codec (gcow_amd.dist.DeviceCodec); tests inject an oracle-backed codec to run the hook bodies over gloo.
 """
 import contextlib
@@ -53,6 +54,9 @@ class GcowHookState:
     process_group: object = None
     codec: object = None  # None: gcow_amd.dist.device_codec()
     timeout_s: float = 300.0
+    # the state is registered with compressed_sharded_hook (its exchange runs on the comm thread at any rate); set by
+    # make_hook_state(hook=compressed_sharded_hook)
+    sharded: bool = False
     _worker: object = field(default=None, repr=False)
     _side: dict = field(default_factory=dict, repr=False)
     _comm_group: object = field(default=None, repr=False)
@@ -66,9 +70,11 @@ class GcowHookState:
         return self._worker
 
     def needs_comm_group(self) -> bool:
-        """An exchange group exists for every multi-rank state: the variable-rate all-gather hook and the sharded
-        hook (any rate) run their collectives on the comm thread over it."""
-        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.process_group) > 1
+        """A multi-rank state whose hook runs collectives on the comm thread: variable rate (the all-gather hook's
+        length exchange) or the sharded hook at any rate. The fixed-rate all-gather and round-trip hooks issue theirs
+        from the autograd thread on `process_group` and get no extra communicator."""
+        return (dist.is_available() and dist.is_initialized() and dist.get_world_size(self.process_group) > 1
+                and (self.sharded or not _codec.is_fixed(self.params)))
 
     def setup(self) -> "GcowHookState":
         """Create the exchange's process group (a collective over `process_group`'s ranks; a no-op for a one-rank
@@ -86,8 +92,10 @@ class GcowHookState:
         with process-group creation on the main thread, and creating it in the hook would block the autograd thread
         until every rank reached that bucket."""
         if self._comm_group is None:
-            raise RuntimeError("GcowHookState.setup() was not called: the variable-rate exchange needs its process "
-                               "group, created by setup() on every rank before training (or use make_hook_state)")
+            raise RuntimeError("GcowHookState has no exchange group: the variable-rate and sharded exchanges need "
+                               "one, created by setup() on every rank before training -- use "
+                               "make_hook_state(hook=<the hook>, ...), or GcowHookState(..., sharded=True).setup() "
+                               "for compressed_sharded_hook")
         return self._comm_group
 
     def _abort_comm_group(self, ex):
@@ -108,8 +116,11 @@ class GcowHookState:
         return self._side[dev]
 
 
-def make_hook_state(**kw) -> GcowHookState:
-    """GcowHookState(**kw).setup(): call on every rank of the hook's process group at the same point of setup."""
+def make_hook_state(hook=None, **kw) -> GcowHookState:
+    """GcowHookState(**kw).setup() for `hook` (the function the state is registered with; compressed_sharded_hook
+    sets `sharded`): call on every rank of the hook's process group at the same point of setup."""
+    if hook is not None and getattr(hook, "__name__", "") == "compressed_sharded_hook":
+        kw.setdefault("sharded", True)
     return GcowHookState(**kw).setup()
 
 

@@ -227,13 +227,16 @@ def shard_pieces_fixed(words: torch.Tensor, nvals: int, maxbits: int, group=None
     """Fixed rate: this rank's stream cut at the shard boundaries and exchanged. Returns (pieces, piece_words, lo,
     hi): pieces holds rank s's piece of this rank's shard at s * piece_words (+ 2 zero words), [lo, hi) the shard."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    bounds, per = shard_plan(nvals, world)
-    pw = max(1, (per // 4) * maxbits // 64)
+    bounds, _ = shard_plan(nvals, world)
     nb = (nvals + 3) // 4
+    # piece r = the words holding shard r's blocks: from the word its first block starts in (a 64-block multiple of
+    # maxbits bits is whole words) to the word its last bit falls in -- a partial last block and a shard whose bits
+    # are not a multiple of 64 (the last shard, or a one-shard bucket) end inside a word that must travel too
+    spans = [((lo // 4) * maxbits // 64, (min((hi + 3) // 4, nb) * maxbits + 63) // 64) if hi > lo else (0, 0)
+             for lo, hi in bounds]
+    pw = max(1, max(w1 - w0 for w0, w1 in spans))
     send = torch.zeros(world * pw, dtype=torch.int64, device=words.device)
-    for r, (lo, hi) in enumerate(bounds):
-        w0 = (lo // 4) * maxbits // 64
-        w1 = (min((hi + 3) // 4, nb) * maxbits + 63) // 64
+    for r, (w0, w1) in enumerate(spans):
         if w1 > w0:
             send[r * pw:r * pw + (w1 - w0)] = words[w0:w1]
     pieces = torch.zeros(world * pw + 2, dtype=torch.int64, device=words.device)
@@ -254,7 +257,8 @@ def shard_pieces_variable(words: torch.Tensor, bits, index: torch.Tensor, nvals:
     bounds, per = shard_plan(nvals, world)
     dev = words.device
     nb = (nvals + 3) // 4
-    assert SHARD_ALIGN_BLOCKS % index_stride == 0
+    if index_stride not in (8, 16):  # the block-index spacings gcow_decode_mean_device takes
+        raise GcowError("shard_pieces_variable: index_stride must be 8 or 16, got %r" % (index_stride,))
     starts = [lo // 4 // index_stride for lo, _ in bounds]  # index chunk of each shard's first block
     bits_t = bits.reshape(1).to(device=dev, dtype=torch.int64) if isinstance(bits, torch.Tensor) else \
         torch.tensor([int(bits)], dtype=torch.int64, device=dev)

@@ -33,12 +33,14 @@ def test_bench_self_launches_n_ranks(n):
     assert d["n_gpus"] == n
     assert sorted(tuple(r[:3]) for r in d["ranks"]) == [(i, i, n) for i in range(n)]
     assert all(r[3] == "self" for r in d["ranks"])
+    # one rendezvous on the loopback address, at the port torchrun's own store bound (not one picked beforehand)
+    assert len({(r[4], r[5]) for r in d["ranks"]}) == 1 and d["ranks"][0][4] == "127.0.0.1"
     assert d["steps"] == 3 and d["warmup"] == 1 and d["ms_per_step"] > 0
 
 
 def test_bench_single_rank():
     d = _run("--gpus", "1")
-    assert d["n_gpus"] == 1 and d["ranks"] == [[0, 0, 1, "torchrun"]]
+    assert d["n_gpus"] == 1 and d["ranks"][0][:4] == [0, 0, 1, "torchrun"]
 
 
 def test_bench_programmatic_argv_reaches_ranks():
@@ -78,3 +80,14 @@ def test_parity_failures_scan():
     line = {"a": {"gathered_stream_matches_oracle": True}, "c5_sharded": {"stitched_stream_matches_oracle": False},
             "legs": [{"x_matches_oracle": None}, {"y_matches_oracle": False}]}
     assert bench.parity_failures(line) == ["c5_sharded.stitched_stream_matches_oracle", "legs.1.y_matches_oracle"]
+
+
+def test_launcher_lets_torchrun_pick_the_port():
+    """the N > 1 launcher used to bind port 0, read the port, close it and pass it as --master-port, a
+    window in which another job could take it. It now asks torchrun for a standalone rendezvous on 127.0.0.1."""
+    sys.path.insert(0, ROOT)
+    import bench
+    cmd = bench.launcher_cmd(8, ["--gpus", "8"])
+    assert "--standalone" in cmd and "--local-addr=127.0.0.1" in cmd and "--nproc-per-node=8" in cmd
+    assert not any(a.startswith("--master-port") for a in cmd)
+    assert cmd[-2:] == ["--gpus", "8"]

@@ -110,7 +110,8 @@ def _hook_worker(rank, world, port, q, hook_name, mode):
         ref.load_state_dict(model.state_dict())
         dm = nn.parallel.DistributedDataParallel(model)
         p = _params(mode)
-        dm.register_comm_hook(ddp.make_hook_state(params=p, codec=OracleCodec()), getattr(ddp, hook_name))
+        hook = getattr(ddp, hook_name)
+        dm.register_comm_hook(ddp.make_hook_state(hook=hook, params=p, codec=OracleCodec()), hook)
         torch.manual_seed(100 + rank)  # a different batch per rank
         x = torch.randn(16, 53)
         dm(x).square().mean().backward()
@@ -338,7 +339,11 @@ def _state_setup_worker(rank, world, port, q):
             ok = "setup()" in str(ex)
         st.setup()
         ok = ok and st.comm_group() is not None and st.setup().comm_group() is st.comm_group()  # idempotent
-        ok = ok and ddp.GcowHookState(params=_params("rate16")).setup()._comm_group is not None  # any rate
+        # the sharded hook's state has a group at any rate; a fixed-rate all-gather / round-trip state needs none
+        ok = ok and ddp.make_hook_state(hook=ddp.compressed_sharded_hook, params=_params("rate16"))._comm_group \
+            is not None
+        ok = ok and ddp.make_hook_state(hook=ddp.compressed_allgather_hook, params=_params("rate16"))._comm_group \
+            is None
         q.put((rank, True if ok else "rank %d: setup semantics" % rank))
     except Exception as ex:  # pragma: no cover
         q.put((rank, repr(ex)))
@@ -445,3 +450,13 @@ def test_sharded_pieces_index8_gloo(world, mode, nvals, bf16):
     """The same exchange with the block index every 8 blocks (the sharded hook's spacing, ddp.SHARDED_INDEX_STRIDE):
     pieces cut and index slices rebased at 8-block granularity, bit for bit against the oracle mean."""
     _run(_sharded_exchange_worker, world, mode, nvals, bf16, 8)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("mode", ["rate16", "rate8", "rate2.5"])
+@pytest.mark.parametrize("nvals", [10, 29, 4 * 63 + 3])
+def test_sharded_pieces_fixed_small_buckets(world, mode, nvals):
+    """Fixed-rate buckets of 64 blocks or fewer: one rank owns the whole bucket, and its bits (a partial last block,
+    or blocks * maxbits not a multiple of 64) end inside a word. The piece must carry that word (the piece
+    size was floor((values // 4) * maxbits / 64) words, one short at rate 8 / 2.5)."""
+    _run(_sharded_exchange_worker, world, mode, nvals, False)

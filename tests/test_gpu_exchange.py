@@ -9,7 +9,6 @@
 * both DDP hooks at world 1 over RCCL, each gradient compared bit-exactly with the oracle.
 """
 import os
-import socket
 import tempfile
 import sys
 
@@ -299,14 +298,6 @@ class HostStagedDeviceCodec:
         return out.copy_(o) if out is not None else o
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _mp_worker(rank, world, port, q, what, mode):
     import torch.distributed as dist
     for p in (ROOT, os.path.join(ROOT, "tests")):
@@ -320,8 +311,10 @@ def _mp_worker(rank, world, port, q, what, mode):
         p = {"rate16": codec.rate(16, 1), "acc1e-6": codec.accuracy(1e-6), "bf16_acc1e-3": codec.accuracy(1e-3)}[mode]
         op = O.expert(*p.tuple())
         cdc = HostStagedDeviceCodec()
-        if what == "encode_allgather":
-            a = O.gen_normal(4 * 30011 + 1, 1e-3, 5, True)
+        if what.startswith("encode_allgather"):
+            # "_equal": 8 x 6400 values, equal 16-block-aligned shards at world 8 (the C4 layout: one all-gather of the
+            # shard streams is the stream); otherwise ragged shards and a partial last block (stitched)
+            a = O.gen_normal(8 * 6400 if what.endswith("_equal") else 4 * 30011 + 1, 1e-3, 5, True)
             if mode.startswith("bf16"):
                 a = (a.view(np.uint32) >> 16).astype(np.uint16)
                 bucket = torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16)
@@ -333,14 +326,17 @@ def _mp_worker(rank, world, port, q, what, mode):
         else:
             import torch.nn as nn
             torch.manual_seed(0)
-            model = nn.Linear(67, 61, bias=False)
-            refm = nn.Linear(67, 61, bias=False)
+            # 4087 values = 1022 blocks (world 8: seven 128-block shards and a ragged one ending in a partial block);
+            # "_small": 600 values = 150 blocks, so at world 8 ranks 3..7 own empty shards
+            fi, fo = (20, 30) if what.endswith("_small") else (67, 61)
+            model = nn.Linear(fi, fo, bias=False)
+            refm = nn.Linear(fi, fo, bias=False)
             refm.load_state_dict(model.state_dict())
             dm = nn.parallel.DistributedDataParallel(model)
-            hook = ddp.compressed_sharded_hook if what == "sharded_hook" else ddp.compressed_allgather_hook
-            dm.register_comm_hook(ddp.make_hook_state(params=p, codec=cdc), hook)
+            hook = ddp.compressed_sharded_hook if what.startswith("sharded_hook") else ddp.compressed_allgather_hook
+            dm.register_comm_hook(ddp.make_hook_state(hook=hook, params=p, codec=cdc), hook)
             torch.manual_seed(10 + rank)
-            x = torch.randn(8, 67)
+            x = torch.randn(8, fi)
             dm(x).square().mean().backward()
             refm(x).square().mean().backward()
             g = refm.weight.grad.reshape(-1).contiguous()
@@ -364,6 +360,22 @@ def _mp_worker(rank, world, port, q, what, mode):
                                        ("sharded_hook", "rate16"), ("sharded_hook", "acc1e-6")])
 @pytest.mark.parametrize("world", [2, 3])
 def test_exchange_multiprocess_device_codec(gc, what, mode, world):
+    _run_mp(what, mode, world)
+
+
+@pytest.mark.parametrize("what,mode", [("encode_allgather_equal", "rate16"), ("encode_allgather", "rate16"),
+                                       ("encode_allgather", "bf16_acc1e-3"), ("sharded_hook", "acc1e-6"), ("sharded_hook_small", "acc1e-6"),
+                                       ("sharded_hook_small", "rate16"), ("hook", "acc1e-6")])
+def test_exchange_multiprocess_device_codec_world8(gc, what, mode):
+    """The C4 / C5-8-GPU exchange shape: 8 processes sharing the one GPU, every codec call on the gfx950
+    kernels, the collectives over gloo. encode_allgather at rate 16 (equal 16-block-aligned shards: one all-gather;
+    ragged shards: stitched) and bf16 accuracy 1e-3 (length exchange, padded all-gather, one-launch stitch) must equal the
+    oracle's single-stream encode; the sharded hook at accuracy 1e-6 with a ragged last shard, and with ranks 3..7
+    owning empty shards, must give every rank the oracle's mean of decode(encode(g_r)) bit for bit."""
+    _run_mp(what, mode, 8, timeout=300)
+
+
+def _run_mp(what, mode, world, timeout=100):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -372,9 +384,13 @@ def test_exchange_multiprocess_device_codec(gc, what, mode, world):
         procs = [ctx.Process(target=_mp_worker, args=(r, world, init, q, what, mode)) for r in range(world)]
         for pr in procs:
             pr.start()
-        res = [q.get(timeout=100) for _ in procs]
-        for pr in procs:
-            pr.join(timeout=60)
+        try:
+            res = [q.get(timeout=timeout) for _ in procs]
+        finally:
+            for pr in procs:
+                pr.join(timeout=60)
+                if pr.is_alive():
+                    pr.kill()
     assert all(ok is True for _, ok in res), res
 
 
@@ -442,7 +458,7 @@ def test_ddp_allgather_hook_bf16_world1(gc, orc, nccl_world1, mode, hook):
     model, ref = layers(), layers()
     ref.load_state_dict(model.state_dict())
     dm = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=1)
-    dm.register_comm_hook(ddp.make_hook_state(params=params), getattr(ddp, hook))
+    dm.register_comm_hook(ddp.make_hook_state(hook=getattr(ddp, hook), params=params), getattr(ddp, hook))
     op = orc.expert(*params.tuple())
     for step in range(2):
         model.zero_grad()

@@ -1,0 +1,60 @@
+"""Why the first C5 host-path leg of a process is slow (11.7 -> 20.8 ms once the host legs moved
+after the device legs). Per-step times of HostEncoder(chunks=16) on the 256 Mi bf16 C5 bucket at accuracy 1e-6 under:
+  fresh      h_in = xb.cpu().pin_memory(), h_out = torch.empty(pin_memory=True) (the bench's order), 10 steps
+  again      the same buffers, 10 more steps
+  touched    a NEW pinned h_out written once by the CPU (zero_) before the first step
+  h2d / d2h  the bare copies of the whole bucket / stream on fresh pinned buffers, per step
+"""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from gcow_amd import codec  # noqa: E402
+
+dev = torch.device("cuda", 0)
+n = 256 << 20
+x32 = torch.empty(n, dtype=torch.float32, device=dev)
+codec.fill_normal(x32, 1e-3, seed=0x67636F77, inject=True)
+xb = x32.to(torch.bfloat16)
+del x32
+p = codec.accuracy(1e-6)
+cap = codec.max_output_bytes((n,), p, torch.bfloat16) // 8 + 2
+
+
+def steps(name, fn, k=10):
+    ts = []
+    for _ in range(k):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    print("%-22s %s" % (name, " ".join("%.2f" % t for t in ts)), flush=True)
+
+
+mode = sys.argv[1] if len(sys.argv) > 1 else "all"
+if mode in ("all", "copies"):
+    a = xb.cpu().pin_memory()
+    steps("h2d fresh", lambda: xb.copy_(a, non_blocking=True))
+    o = torch.empty(cap, dtype=torch.int64, pin_memory=True)
+    w = torch.empty(n // 4, dtype=torch.int64, device=dev)
+    steps("d2h fresh", lambda: o[: n // 4].copy_(w, non_blocking=True))
+    o2 = torch.empty(cap, dtype=torch.int64)
+    o2.zero_()
+    o2 = o2.pin_memory()
+    steps("d2h pre-touched", lambda: o2[: n // 4].copy_(w, non_blocking=True))
+    del a, o, o2, w
+if mode in ("all", "host"):
+    h_in = xb.cpu().pin_memory()
+    h_out = torch.empty(cap, dtype=torch.int64, pin_memory=True)
+    henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=16, device=dev)
+    steps("host fresh", lambda: henc(h_in, h_out))
+    steps("host again", lambda: henc(h_in, h_out))
+    h_out2 = torch.empty(cap + 1, dtype=torch.int64, pin_memory=True)
+    h_out2.zero_()
+    steps("host out touched", lambda: henc(h_in, h_out2))
+    h_in2 = torch.empty(n + 8, dtype=torch.bfloat16, pin_memory=True)
+    h_in2[:n].copy_(h_in)
+    steps("host in re-pinned", lambda: henc(h_in2[:n], h_out))
