@@ -125,11 +125,17 @@ class Ctx:
         return t.tolist()
 
 
-def timed(ctx: Ctx, step, warmup: int, steps: int, group=None, stream=None):
+def timed(ctx: Ctx, step, warmup: int, steps: int, group=None, stream=None, walls=None):
     """W untimed steps, then exactly K steps bracketed by barrier + synchronize on both sides. Returns (wall ms per
-    step, per-step kernel ms from HIP events on `stream` -- [] in stub mode)."""
-    for _ in range(warmup):
+    step, per-step kernel ms from HIP events on `stream` -- [] in stub mode). `walls` (a list) receives the host wall
+    ms of every call, warmup included (meaningful for steps that synchronise themselves, e.g. HostEncoder)."""
+    def call():
+        t = time.perf_counter()
         step()
+        if walls is not None:
+            walls.append(round((time.perf_counter() - t) * 1e3, 3))
+    for _ in range(warmup):
+        call()
     ctx.sync()
     ctx.barrier(group)
     ctx.sync()
@@ -140,7 +146,7 @@ def timed(ctx: Ctx, step, warmup: int, steps: int, group=None, stream=None):
     if evs:
         evs[0].record(stream)
     for i in range(steps):
-        step()
+        call()
         if evs:
             evs[i + 1].record(stream)
     ctx.sync()
@@ -471,14 +477,30 @@ def leg_host_e2e(ctx, enc, x, p, n, in_bytes, out_bytes):
         e = enc(x)
         h_out[:nwo].copy_(e.words[:nwo], non_blocking=True)
 
-    h_ms, _ = timed(ctx, seq, 2, 5)
+    settle_host(lambda: (seq(), ctx.sync()))
+    h_ms, _ = timed(ctx, seq, 0, 5)
     henc = codec.HostEncoder(n, torch.float32, p, chunks=16, device=ctx.dev)
-    o_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 2, 5)
+    settle_host(lambda: henc(h_in, h_out), 0.25)
+    o_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 0, 5)
     ok = host_stream_check(henc, h_in, h_out, p)
     return {"ms_per_step": round(h_ms, 3), "GiBps_input": round(gib(in_bytes, h_ms), 2),
             "overlapped_ms_per_step": round(o_ms, 3), "overlapped_GiBps_input": round(gib(in_bytes, o_ms), 2),
             "host_stream_matches_oracle": ok,
             "note": "pinned H2D + encode + D2H, PCIe-inclusive (not `value`); overlapped: 16 chunks on 3 streams"}
+
+
+def settle_host(step, seconds: float = 1.0) -> list:
+    """Untimed calls of a host-resident step (it synchronises itself) for `seconds` of wall time, at least two; returns
+    their wall ms. After a long GPU-only phase the first ~0.55 s of PCIe traffic runs its D2H copies at about half
+    rate whatever the copy issue order or buffers (profiles/r06_host_path_transient.log: 19.3 ms per call, then 11.8
+    from one call to the next, ~0.55 s in), so a count of warmup calls is not a warm state."""
+    walls = []
+    t_end = time.perf_counter() + seconds
+    while len(walls) < 2 or time.perf_counter() < t_end:
+        t = time.perf_counter()
+        step()
+        walls.append(round((time.perf_counter() - t) * 1e3, 3))
+    return walls
 
 
 def oracle_threads() -> int:
@@ -636,9 +658,12 @@ def leg_configs(ctx):
         h_out = torch.empty(codec.max_output_bytes((n,), p, torch.bfloat16) // 8 + 2, dtype=torch.int64,
                             pin_memory=True)
         henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=16, device=ctx.dev)
-        h_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 2, 5)
+        sw = settle_host(lambda: henc(h_in, h_out))
+        hw = []
+        h_ms, _ = timed(ctx, lambda: henc(h_in, h_out), 0, 5, walls=hw)
         h_ok = host_stream_check(henc, h_in, h_out, p)
         out[name].update({"host_path_ms": round(h_ms, 3), "host_path_GiBps_input": round(gib(n * 2, h_ms), 2),
+                          "host_path_calls_ms": hw, "host_path_settle_calls_ms": sw[:12],
                           "host_path_stream_matches_oracle": h_ok,
                           "host_path_note": "pinned bf16 H2D + encode + D2H, 16 overlapped chunks (PCIe-bound)"})
         del h_out, henc
@@ -653,7 +678,7 @@ def exact_stream(e):
     return codec.Encoded(e.stream(), e.bits_dev, e.shape, e.params, e.index, e.index_stride)
 
 
-def leg_decode_mean(ctx, W: int = 8):
+def leg_decode_mean(ctx, W: int = 8, names=("rate16", "acc1e-6")):
     """The receive side of gcow_amd.ddp.compressed_allgather_hook on one GPU: W = 8 ranks' streams of 256 Mi fp32
     values (W different buckets of the bench distribution) decoded and averaged in one launch (codec.decode_mean), at
     rate 16 (the caller's default rate, hw/models/train_imagenet.py:155) and accuracy 1e-6 (the caller's default
@@ -665,6 +690,8 @@ def leg_decode_mean(ctx, W: int = 8):
     st = torch.cuda.current_stream(ctx.dev)
     res = {}
     for name, p, stride in (("rate16", codec.rate(16, 1), 0), ("acc1e-6", codec.accuracy(1e-6), 16)):
+        if name not in names:
+            continue
         # variable rate: encoded with the sharded hook's index (every 8 blocks); the all-gather hook's index (every 16
         # blocks) is every other entry of it -- the stream words do not depend on the spacing
         sstride = ddp.SHARDED_INDEX_STRIDE if stride else 0

@@ -58,3 +58,20 @@ if mode in ("all", "host"):
     h_in2 = torch.empty(n + 8, dtype=torch.bfloat16, pin_memory=True)
     h_in2[:n].copy_(h_in)
     steps("host in re-pinned", lambda: henc(h_in2[:n], h_out))
+if mode == "streams":
+    # does the steady host-path time depend on which pool streams (-> which hardware queues) HostEncoder gets?
+    h_in = xb.cpu().pin_memory()
+    h_out = torch.empty(cap, dtype=torch.int64, pin_memory=True)
+    held = []
+    for k in range(8):
+        henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=16, device=dev)
+        steps("pool offset %d" % (3 * k), lambda: henc(h_in, h_out), 6)
+        del henc
+    henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=16, device=dev)
+    henc.s_d2h = henc.s_h2d
+    steps("h2d stream == d2h stream", lambda: henc(h_in, h_out), 6)
+    for k in range(4):
+        henc = codec.HostEncoder(n, torch.bfloat16, p, chunks=16, device=dev)
+        extra = torch.cuda.Stream(dev)
+        henc.s_d2h = extra
+        steps("d2h on +1 stream %d" % k, lambda: henc(h_in, h_out), 6)
