@@ -393,9 +393,8 @@ class HostEncoder:
     chunk i at its known word offset. Only whole 64-bit words that no later chunk touches are copied back early.
     The result is byte-identical to one device encode of the whole bucket."""
 
-    def __init__(self, n: int, dtype, params: GcowParams, chunks: int = 8, device=None, issue_ahead: bool = True):
+    def __init__(self, n: int, dtype, params: GcowParams, chunks: int = 8, device=None):
         self.n, self.dtype, self.params = int(n), dtype, params
-        self.issue_ahead = issue_ahead
         self.device = torch.device(device or "cuda")
         self.fixed = is_fixed(params)
         nb = (self.n + 3) // 4
@@ -464,20 +463,13 @@ class HostEncoder:
                 with torch.cuda.stream(self.s_enc):
                     self.h_bits[i + 1:i + 2].copy_(self.d_bits[i + 1:i + 2], non_blocking=True)
             ev_enc[i].record(self.s_enc)
-            if i >= 1 and (self.fixed or not self.issue_ahead):
-                # chunk i-1's complete words (chunk i only ORs into the word its first bit falls in)
+            if i >= 1:  # chunk i-1's complete words (chunk i only ORs into the word its first bit falls in)
                 if self.fixed:
                     end = (self.bounds[i - 1][1] + 3) // 4 * p.maxbits
                 else:
                     ev_enc[i - 1].synchronize()
                     end = int(self.h_bits[i])
                 copy_back(end // 64, ev_enc[i - 1])
-        if not self.fixed and self.issue_ahead:
-            # every H2D copy and encode is already queued (stream waits only); the host now learns each chunk's end as
-            # its encode completes and queues that D2H copy -- no H2D copy waits behind a host read
-            for i in range(1, k):
-                ev_enc[i - 1].synchronize()
-                copy_back(int(self.h_bits[i]) // 64, ev_enc[i - 1])
         if self.fixed:
             bits = ((self.n + 3) // 4) * p.maxbits
         else:
