@@ -404,10 +404,9 @@ def leg_hook_exchange(ctx, n):
     codec.fill_normal(x, 1e-3, seed=SEED + 77 + ctx.rank, inject=True)
     out = {}
     for name, p, stride in (("rate16", codec.rate(16, 1), 0), ("acc1e-6", codec.accuracy(1e-6), 16)):
-        enc = codec.Encoder((n,), torch.float32, p, ctx.dev, index_stride=stride)
-        # the sharded hook's own index spacing (ddp.SHARDED_INDEX_STRIDE); the stream words are the same
+        # both hooks encode with the 8-block index (ddp.SHARDED_INDEX_STRIDE); the all-gather hook sends it packed
         sstride = ddp.SHARDED_INDEX_STRIDE if stride else 0
-        senc = codec.Encoder((n,), torch.float32, p, ctx.dev, index_stride=sstride) if stride else enc
+        enc = senc = codec.Encoder((n,), torch.float32, p, ctx.dev, index_stride=sstride)
         ag = torch.empty(n, dtype=torch.float32, device=ctx.dev)
         sh = torch.empty(n, dtype=torch.float32, device=ctx.dev)
 
@@ -417,10 +416,11 @@ def leg_hook_exchange(ctx, n):
                 _, lens_h = gdist.gather_lengths(e.bits_dev, ctx.dev)
                 sw = max(1, max((b + 63) // 64 for b in lens_h))
                 g = gdist.allgather_padded(e.words, (lens_h[ctx.rank] + 63) // 64, sw, pad=2)
-                ni = e.index.numel()
+                pk = codec.pack_index16(e.index, n, p)
+                ni = pk.numel()
                 idx = torch.empty(W * ni, dtype=torch.int64, device=ctx.dev)
-                gdist.allgather_into(idx, e.index[:ni].contiguous())
-                codec.decode_mean(g, sw, W, n, p, idx, ni, stride, out=ag)
+                gdist.allgather_into(idx, pk)
+                codec.decode_mean(g, sw, W, n, p, idx, ni, codec.INDEX_PACKED16, out=ag)
             else:
                 nw = ((n + 3) // 4 * p.maxbits + 63) // 64
                 g = torch.zeros(W * nw + 2, dtype=torch.int64, device=ctx.dev)
@@ -710,18 +710,25 @@ def leg_decode_mean(ctx, W: int = 8, names=("rate16", "acc1e-6")):
             buf[r * sw:r * sw + t.numel()] = t
         ix8 = torch.cat(idx) if stride else None
         ni8 = idx[0].numel() if stride else 0
-        ix = ix8.view(W, ni8)[:, ::stride // sstride].contiguous().view(-1) if stride else None
-        ni = ix.numel() // W if stride else 0
+        # the all-gather hook's index (ddp.compressed_allgather_hook): every 8 blocks, packed into 16-block entries
+        ixp = torch.cat([codec.pack_index16(t, n, p) for t in idx]) if stride else None
+        nip = ixp.numel() // W if stride else 0
         del parts, idx, enc
-        _, per = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ix, ni, stride, out=mean, stream=st), 3, 10,
+        kp = codec.INDEX_PACKED16 if stride else 0
+        _, per = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ixp, nip, kp, out=mean, stream=st), 3, 10,
                        stream=st)
         k = sum(per) / len(per)
-        k8 = None
-        if stride:  # the same decode with the sharded hook's index spacing (8-block chunks)
+        k8 = k16 = None
+        if stride:  # the same decode with the plain 8-block index, and with a plain 16-block index (16-block chunks)
             _, per8 = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ix8, ni8, sstride, out=mean, stream=st), 3,
                             10, stream=st)
             k8 = round(sum(per8) / len(per8), 4)
-        kname = "k_decode_mean_fixed1d<64>" if stride == 0 else "k_decode_mean1d_var<128>"
+            ix16 = ix8.view(W, ni8)[:, ::stride // sstride].contiguous().view(-1)
+            _, per16 = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ix16, ix16.numel() // W, stride, out=mean,
+                                                            stream=st), 3, 10, stream=st)
+            k16 = round(sum(per16) / len(per16), 4)
+            del ix16
+        kname = "k_decode_mean_fixed1d_np<64>" if stride == 0 else "k_decode_mean1d_var_lean<128, 64, 8, packed16>"
         # the sharded receive (ddp.compressed_sharded_hook): one rank's decode-mean of its 1/W shard from the W pieces
         # the all-to-all delivers (cut here from the same streams; the exchange itself is an N > 1 leg)
         pieces, pw, pidx, iw, lo, hi = shard0_pieces(buf, sw, W, n, p, ix8, ni8, sstride or 16)
@@ -731,10 +738,11 @@ def leg_decode_mean(ctx, W: int = 8, names=("rate16", "acc1e-6")):
         ks = sum(sper) / len(sper)
         res[name] = {"streams": W, "values": n, "kernel_ms": round(k, 4), "bits_per_value": round(bits / W / n, 3),
                      "roofline": roof(bits / 8, n * 4, k, kname, basis="write"),
-                     "kernel_ms_index_stride8": k8,
+                     "index": "packed16 (8-block chunks)" if stride else None,
+                     "kernel_ms_index_stride8": k8, "kernel_ms_index_stride16": k16,
                      "sharded_receive_kernel_ms": round(ks, 4), "sharded_receive_values": hi - lo,
-                     "index_stride": stride, "sharded_index_stride": sstride}
-        del buf, ix, ix8, pieces, pidx
+                     "sharded_index_stride": sstride}
+        del buf, ixp, ix8, pieces, pidx
         torch.cuda.empty_cache()
     del x, mean
     return res

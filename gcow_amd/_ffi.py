@@ -107,6 +107,7 @@ def load():
         "gcow_stitch_device": (i32, [vp, u64, vp, u64, vp]),
         "gcow_stitch_shards_device": (i32, [vp, u64, vp, u64, vp, u32, vp]),
         "gcow_decode_mean_device": (i32, [pi, pp, vp, sz, u64, u32, vp, u64, u32, vp]),
+        "gcow_index_pack16_device": (i32, [pi, pp, vp, vp, vp]),
         "gcow_header_bits": (C.c_uint, [pp]),
         "gcow_write_header": (C.c_uint, [pi, pp, P(u64)]),
         "gcow_read_header": (C.c_uint, [P(u64), sz, pi, pp]),

@@ -17,6 +17,8 @@ import torch
 from ._ffi import DTYPE_BF16, DTYPE_FLOAT, GcowError, GcowParams, ZfpInput, check, load
 
 ZFP_MIN_BITS, ZFP_MAX_BITS, ZFP_MAX_PREC, ZFP_MIN_EXP = 1, 16658, 64, -1074
+# index_stride of decode_mean for the packed 16-block index (include/gcow.h GCOW_INDEX_PACKED16)
+INDEX_PACKED16 = 0x1010
 
 
 # ------------------------------------------------------------------------------------------- parameters
@@ -240,6 +242,22 @@ def decode_mean(streams: torch.Tensor, stream_words: int, nstreams: int, n: int,
                                          index.data_ptr() if index is not None else None, index_words, index_stride,
                                          _stream_ptr(stream)), "gcow_decode_mean_device")
     return out
+
+
+def pack_index16(index8: torch.Tensor, n: int, params: GcowParams, out: torch.Tensor | None = None,
+                 stream=None) -> torch.Tensor:
+    """The packed 16-block index (gcow_index_pack16_device) of one stream of n values from its index every 8 blocks:
+    ceil(n / 64) int64 entries, low 48 bits block 16 c's bit position, high 16 bits block 16 c + 8's offset from it.
+    decode_mean(..., index_stride=INDEX_PACKED16) reads it as 8-block chunks."""
+    n16 = (n + 63) // 64
+    if out is None:
+        out = torch.empty(max(n16, 1), dtype=torch.int64, device=index8.device)
+    if out.numel() < n16 or index8.numel() < (n + 31) // 32 or not (index8.is_cuda and out.is_cuda):
+        raise GcowError("pack_index16: device index of ceil(n / 32) entries and an output of ceil(n / 64)")
+    f = field_of_shape((n,), torch.float32)
+    check(load().gcow_index_pack16_device(C.byref(f), C.byref(params), index8.data_ptr(), out.data_ptr(),
+                                          _stream_ptr(stream)), "gcow_index_pack16_device")
+    return out[:n16] if n16 else out[:0]
 
 
 def fill_normal(out: torch.Tensor, sigma: float = 1e-3, seed: int = 0x67636F77, inject: bool = True, stream=None):

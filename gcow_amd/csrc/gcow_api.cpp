@@ -988,9 +988,9 @@ gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p
   if (streams_bytes / 8 < (uint64_t)nstreams * stream_words + 2)
     return fail(GCOW_ERR_INVALID, "stream buffer smaller than nstreams * stream_words + 2 words");
   if (p->minbits != p->maxbits) {
-    if (!d_index || (index_stride != 8 && index_stride != 16) ||
-        index_words < (F.nblocks + index_stride - 1) / index_stride)
-      return fail(GCOW_ERR_INVALID, "variable-rate decode_mean needs each stream's index (stride 8 or 16)");
+    const uint32_t per = index_stride == GCOW_INDEX_PACKED16 ? 16u : index_stride;
+    if (!d_index || (per != 8 && per != 16) || index_words < (F.nblocks + per - 1) / per)
+      return fail(GCOW_ERR_INVALID, "variable-rate decode_mean needs each stream's index (stride 8 or 16, or packed16)");
   } else {
     if (d_index || index_stride || index_words)
       return fail(GCOW_ERR_INVALID, "fixed-rate decode_mean takes no block index (blocks are at b * maxbits)");
@@ -999,6 +999,25 @@ gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p
   }
   GCOW_HIP(gcow::launch_decode_mean1d(F, P(*p), d_streams, stream_words, nstreams, d_index, index_words, hip_stream,
                                       index_stride ? index_stride : 16));
+  return GCOW_OK;
+}
+
+gcow_status gcow_index_pack16_device(const zfp_input* field, const gcow_params* p, const uint64_t* d_index8,
+                                     uint64_t* d_out, void* hip_stream)
+{
+  if (!field || !p) return fail(GCOW_ERR_INVALID, "null field or params");
+  if (get_input_dimension(field) != 1) return fail(GCOW_ERR_UNSUPPORTED, "packed16 index: 1-D fields only");
+  gcow_status st = check_params(p, 1);
+  if (st) return st;
+  // a 1-D block codes at most 9 + 32 * 4 + 32 + 8 = 177 bits before minbits padding (header, four verbatim bits per
+  // plane, one group flag per plane, the runs and flags of four coefficients turning significant)
+  const uint64_t bmax = std::max<uint64_t>(p->minbits, std::min<uint64_t>(p->maxbits, 177));
+  const uint64_t nb = get_input_num_blocks(field);
+  if (8 * bmax > 0xffff || nb * bmax >= (1ull << 48))
+    return fail(GCOW_ERR_UNSUPPORTED, "packed16 index: 8 blocks may exceed 65535 bits, or the stream 2^48 bits");
+  const uint64_t n8 = (nb + 7) / 8;
+  if (n8 && (!d_index8 || !d_out)) return fail(GCOW_ERR_INVALID, "null index buffer");
+  GCOW_HIP(gcow::launch_index_pack16(d_index8, n8, d_out, hip_stream));
   return GCOW_OK;
 }
 

@@ -2573,12 +2573,28 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
 #ifndef GCOW_DMV_LPAIR
 #define GCOW_DMV_LPAIR 1  // the lean block decoder's group phase through the 16-bit pair table (DecTabLP)
 #endif
+// Block-index readers of the variable-rate decode_mean kernels: plain (one uint64 bit position per index chunk), or
+// packed16 (GCOW_INDEX_PACKED16: one uint64 per 16 blocks -- low 48 bits the position of block 16 c, high 16 bits the
+// offset of block 16 c + 8 from it -- read as the positions of 8-block chunks).
+template <bool PK> struct IndexRd {
+  const uint64_t* ix;
+  __device__ __forceinline__ uint64_t operator[](uint64_t c) const { return ix[c]; }
+};
+template <> struct IndexRd<true> {
+  const uint64_t* ix;
+  __device__ __forceinline__ uint64_t operator[](uint64_t c) const
+  {
+    const uint64_t v = ix[c >> 1];
+    return (v & 0xffffffffffffull) + ((c & 1) ? (v >> 48) : 0ull);
+  }
+};
+
 // Variable rate (1-D closed-form domain), the lean decoder's shape (k_decode1d_var_lean): LANES 16-block chunks per
 // workgroup; for each stream in rank order its span is staged in LDS (in 1, 2 or 4 parts, as there) and each lane
 // decodes its chunk into 64 registers of sums; the means leave through the 8 x 8 lane transposes as whole-line
 // stores. Complete workgroups only (whole chunks, full blocks, contiguous output); the launcher sends the rest to
 // k_decode_mean1d_var.
-template <uint32_t LANES, uint32_t CAPB, uint32_t CH>
+template <uint32_t LANES, uint32_t CAPB, uint32_t CH, bool PK = false>
 __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(CH == 8 ? GCOW_DMV8_WAVES : GCOW_DMV_WAVES, 8))) void k_decode_mean1d_var_lean(FieldDesc F, Params p,
                                                                   const uint64_t* __restrict__ in,
                                                                   uint64_t stream_words,
@@ -2605,7 +2621,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(CH == 8 ?
   for (int k = 0; k < (int)CH; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
   for (uint32_t r = 0; r < nstreams; r++) {
     const uint64_t* sr = in + (uint64_t)r * stream_words;
-    const uint64_t* ix = index + (uint64_t)r * index_words;
+    const IndexRd<PK> ix{index + (uint64_t)r * index_words};
     const uint64_t sbase = (uint64_t)r * stream_words;
     // a span starts on a 16-byte boundary of the whole buffer (streams are stream_words apart, which may be odd):
     // w0 may be one word before this stream's first word (the previous stream's last word, never decoded)
@@ -2671,7 +2687,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(CH == 8 ?
 // Variable rate (1-D closed-form domain) with each stream's block index every 16 blocks (index_words entries apart):
 // the shape of k_decode1d_var_lean -- LANES chunks of 16 blocks per workgroup, the workgroup's span of each stream
 // staged in LDS in turn -- with the 16 blocks' 64 values accumulated in registers across the streams and stored once.
-template <uint32_t LANES, uint32_t CH>
+template <uint32_t LANES, uint32_t CH, bool PK = false>
 __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params p, const uint64_t* __restrict__ in,
                                                              uint64_t stream_words, const uint64_t* __restrict__ index,
                                                              uint64_t index_words, uint64_t nchunks, uint32_t nstreams,
@@ -2691,7 +2707,7 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
   for (int k = 0; k < (int)CH; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
   for (uint32_t r = 0; r < nstreams; r++) {
     const uint64_t* sr = in + (uint64_t)r * stream_words;
-    const uint64_t* ix = index + (uint64_t)r * index_words;
+    const IndexRd<PK> ix{index + (uint64_t)r * index_words};
     // the staged span starts on a 16-byte boundary of the whole buffer (streams are stream_words apart, which may be
     // odd): w0 may be one word before this stream's first word (the previous stream's last word, never decoded)
     const uint64_t sbase = (uint64_t)r * stream_words;
@@ -2741,6 +2757,7 @@ __global__ __launch_bounds__(LANES) void k_decode_mean1d_var(FieldDesc F, Params
 // Variable rate outside the closed-form domain (expert parameters with minbits > 1 or maxbits < 160: a budget can
 // truncate blocks): one lane per 16-block index chunk, the generic libzfp decoder (decode_block) on each stream in
 // rank order, the same fp32 accumulation as above.
+template <bool PK = false>
 __global__ __launch_bounds__(256) void k_decode_mean1d_generic(FieldDesc F, Params p, const uint64_t* __restrict__ in,
                                                                uint64_t stream_words, const uint64_t* __restrict__ index,
                                                                uint64_t index_words, uint64_t nchunks,
@@ -2754,7 +2771,7 @@ __global__ __launch_bounds__(256) void k_decode_mean1d_generic(FieldDesc F, Para
 #pragma unroll
   for (int k = 0; k < 16; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
   for (uint32_t r = 0; r < nstreams; r++) {
-    BitReader rd{in + (uint64_t)r * stream_words, index[(uint64_t)r * index_words + c]};
+    BitReader rd{in + (uint64_t)r * stream_words, IndexRd<PK>{index + (uint64_t)r * index_words}[c]};
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       if (b0 + k < b1) {
@@ -3212,6 +3229,26 @@ hipError_t launch_stitch_shards(uint64_t* dst, uint64_t dst_words, const uint64_
   return hipGetLastError();
 }
 
+// GCOW_INDEX_PACKED16 from an index every 8 blocks: entry c = idx8[2c] | (idx8[2c + 1] - idx8[2c]) << 48 (offset 0
+// where block 16 c + 8 does not exist).
+__global__ __launch_bounds__(256) void k_index_pack16(const uint64_t* __restrict__ idx8, uint64_t n8,
+                                                      uint64_t* __restrict__ out, uint64_t n16)
+{
+  const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (c >= n16) return;
+  const uint64_t a = idx8[2 * c];
+  const uint64_t d = 2 * c + 1 < n8 ? idx8[2 * c + 1] - a : 0ull;
+  out[c] = a | (d << 48);
+}
+
+hipError_t launch_index_pack16(const uint64_t* idx8, uint64_t n8, uint64_t* out, void* stream)
+{
+  const uint64_t n16 = (n8 + 1) / 2;
+  if (!n16) return hipSuccess;
+  k_index_pack16<<<(uint32_t)((n16 + 255) / 256), 256, 0, S(stream)>>>(idx8, n8, out, n16);
+  return hipGetLastError();
+}
+
 hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t stream_words,
                                 uint32_t nstreams, const uint64_t* index, uint64_t index_words, void* stream,
                                 uint32_t chunk)
@@ -3249,12 +3286,18 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
     }
     return hipGetLastError();
   }
-  // variable rate: one lane per index chunk of `chunk` blocks (the streams' index stride, 8 or 16)
+  // variable rate: one lane per index chunk of `chunk` blocks (the streams' index stride, 8 or 16; the packed16
+  // index is read as 8-block chunks)
+  const bool pk = chunk == kIndexPacked16;
+  if (pk) chunk = 8;
   if (chunk != 8 && chunk != 16) return hipErrorInvalidValue;
   const uint64_t nchunks = (F.nblocks + chunk - 1) / chunk;
   if (!(p.minbits <= 1 && p.maxbits >= 160)) {  // a budget can truncate blocks: generic decoder
-    k_decode_mean1d_generic<<<(uint32_t)((nchunks + 255) / 256), 256, 0, st>>>(F, p, in, stream_words, index,
-                                                                              index_words, nchunks, nstreams, chunk);
+    const uint32_t g = (uint32_t)((nchunks + 255) / 256);
+    if (pk) k_decode_mean1d_generic<true><<<g, 256, 0, st>>>(F, p, in, stream_words, index, index_words, nchunks,
+                                                             nstreams, chunk);
+    else k_decode_mean1d_generic<false><<<g, 256, 0, st>>>(F, p, in, stream_words, index, index_words, nchunks,
+                                                           nstreams, chunk);
     return hipGetLastError();
   }
   // complete workgroups (128 whole chunks of full blocks, contiguous output) by the lean kernel, the rest by the
@@ -3264,7 +3307,10 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
     const uint64_t fullchunks = (F.n[0] / 4) / chunk;
     nlean = std::min<uint64_t>(fullchunks, nchunks) / 128;
     if (nlean) {
-      if (chunk == 8)
+      if (pk)
+        k_decode_mean1d_var_lean<128, 64, 8, true><<<(uint32_t)nlean, 128, 0, st>>>(F, p, in, stream_words, index,
+                                                                                    index_words, nchunks, nstreams);
+      else if (chunk == 8)
         k_decode_mean1d_var_lean<128, 64, 8><<<(uint32_t)nlean, 128, 0, st>>>(F, p, in, stream_words, index,
                                                                               index_words, nchunks, nstreams);
       else
@@ -3275,7 +3321,10 @@ hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint6
   const uint64_t cfirst = nlean * 128;
   if (cfirst < nchunks) {
     const uint32_t g = (uint32_t)((nchunks - cfirst + 127) / 128);
-    if (chunk == 8)
+    if (pk)
+      k_decode_mean1d_var<128, 8, true><<<g, 128, 0, st>>>(F, p, in, stream_words, index, index_words, nchunks,
+                                                           nstreams, cfirst);
+    else if (chunk == 8)
       k_decode_mean1d_var<128, 8><<<g, 128, 0, st>>>(F, p, in, stream_words, index, index_words, nchunks, nstreams,
                                                      cfirst);
     else

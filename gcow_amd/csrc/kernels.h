@@ -97,10 +97,14 @@ hipError_t launch_stitch(uint64_t* dst, uint64_t off, const uint64_t* src, uint6
 // all shards of a sharded variable-rate stream in one launch (dst written whole: no zeroing needed)
 hipError_t launch_stitch_shards(uint64_t* dst, uint64_t dst_words, const uint64_t* src, uint64_t shard_words,
                                 const uint64_t* lens, uint32_t nshards, void* stream);
-// mean of nstreams 1-D streams (fixed rate: any params; variable: closed-form domain + index every 16 blocks)
+// GCOW_INDEX_PACKED16 (include/gcow.h): one uint64 per 16 blocks, the 8-block midpoint as a 16-bit offset on top
+constexpr uint32_t kIndexPacked16 = 0x1010u;
+// packed16 index (ceil(n8 / 2) entries) from an index every 8 blocks (n8 entries)
+hipError_t launch_index_pack16(const uint64_t* idx8, uint64_t n8, uint64_t* out, void* stream);
+// mean of nstreams 1-D streams (fixed rate: any params; variable: any params, index every 8 or 16 blocks or packed16)
 hipError_t launch_decode_mean1d(const FieldDesc& F, const Params& p, const uint64_t* in, uint64_t stream_words,
                                 uint32_t nstreams, const uint64_t* index, uint64_t index_words, void* stream,
-                                uint32_t chunk = 16);  // chunk: variable rate's index stride, 8 or 16
+                                uint32_t chunk = 16);  // chunk: variable rate's index stride, 8 or 16, or kIndexPacked16
 hipError_t launch_stage(int which, int dims, const void* a, const void* b, uint32_t n, void* out, uint32_t x0,
                         uint32_t x1, void* out2, uint32_t slot_words, void* stream);
 hipError_t launch_fill_normal(float* out, uint64_t count, double sigma, uint64_t seed, int inject, void* stream);

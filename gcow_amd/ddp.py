@@ -30,11 +30,13 @@ from . import codec as _codec
 from . import dist as gdist
 from ._ffi import GcowParams
 
-INDEX_STRIDE = 16  # block index spacing the multi-stream decoder reads (one entry per 16 blocks)
+INDEX_STRIDE = 16  # block index spacing of the round-trip hook's decode (one entry per 16 blocks)
 # The sharded hook's index spacing: 8 blocks. decode_mean then runs one lane per 8 blocks (32 fp32 sums per lane, no
 # register spills, 5 waves per SIMD): a rank's shard decodes in 0.50 instead of 0.66 ms at W = 8 (accuracy 1e-6,
 # 256 Mi values; profiles/r05_dmean_stride8_ab.log) for an index of 1 byte per block instead of 0.5 -- ~6 % more bytes
-# in the all-to-all. The all-gather hook keeps 16: it gathers every rank's whole index.
+# in the all-to-all. The all-gather hook gathers every rank's whole index, so it encodes with the same 8-block index
+# and sends it packed (codec.pack_index16: the 16-block index's size, the 8-block midpoint as a 16-bit offset), and
+# decode_mean reads the packed entries as 8-block chunks.
 SHARDED_INDEX_STRIDE = 8
 
 
@@ -247,7 +249,8 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
 
         return fut.then(finish)
     cgroup = state.comm_group() if world > 1 else group  # raises here, on the autograd thread, without setup()
-    words, bits, index = cdc.encode(x, p, INDEX_STRIDE, slot=slot)
+    words, bits, index8 = cdc.encode(x, p, SHARDED_INDEX_STRIDE, slot=slot)
+    index = cdc.pack_index16(index8, n, p)  # what travels: one entry per 16 blocks
     dev = x.device
     if dev.type == "cuda":
         ev = torch.cuda.Event()
@@ -274,7 +277,7 @@ def compressed_allgather_hook(state: GcowHookState, bucket) -> torch.futures.Fut
             ni = index.numel()
             idx = torch.empty(world * ni, dtype=torch.int64, device=dev)
             gdist.allgather_into(idx, index[:ni].contiguous(), cgroup)
-            _mean_into(cdc, flat, gathered, maxw, world, n, p, idx, ni, INDEX_STRIDE)
+            _mean_into(cdc, flat, gathered, maxw, world, n, p, idx, ni, _codec.INDEX_PACKED16)
             # completed inside the side-stream context: the future records its event on this stream, so DDP's wait
             # orders its use of the bucket after the mean is written
             fut.set_result(buf)

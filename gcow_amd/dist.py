@@ -75,6 +75,10 @@ class DeviceCodec:
         from . import codec
         return codec.decode(words, (n,), params, index=index, index_stride=index_stride, out=out)
 
+    def pack_index16(self, index8, n: int, params):
+        from . import codec
+        return codec.pack_index16(index8, n, params)
+
     def decode_mean(self, streams, stream_words: int, nstreams: int, n: int, params, index=None,
                     index_words: int = 0, index_stride: int = 0, out=None):
         from . import codec

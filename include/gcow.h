@@ -275,12 +275,27 @@ gcow_status gcow_stitch_shards_device(uint64_t* d_dst, uint64_t dst_words, const
  * + 2 words (the decoders read 64-bit windows past a stream's last bit; GCOW_ERR_INVALID otherwise). Fixed rate: any
  * parameters, d_index NULL and index_words = index_stride = 0. Variable rate: any parameters (minbits <= 1,
  * maxbits >= 160 take the closed-form decoder, others the generic one) and every stream's block index (index_stride
- * 8 or 16, entries index_words apart at d_index, as gcow_encode_device writes them).
+ * 8 or 16, entries index_words apart at d_index, as gcow_encode_device writes them; or GCOW_INDEX_PACKED16, entries
+ * as gcow_index_pack16_device writes them -- the size of the 16-block index, decoded in 8-block chunks).
  */
 gcow_status gcow_decode_mean_device(const zfp_input* field, const gcow_params* p, const uint64_t* d_streams,
                                     size_t streams_bytes, uint64_t stream_words, uint32_t nstreams,
                                     const uint64_t* d_index, uint64_t index_words, uint32_t index_stride,
                                     void* hip_stream);
+
+/*
+ * Packed 16-block index (index_stride GCOW_INDEX_PACKED16 in gcow_decode_mean_device): one uint64 per 16 blocks, the
+ * low 48 bits the stream bit position of block 16 c (as the index every 16 blocks holds it), the high 16 bits the
+ * offset of block 16 c + 8 from it (0 where that block does not exist). It carries the 8-block chunk starts at the
+ * 16-block index's size, so a receiver of every rank's index (the compressed all-gather hook) decodes in 8-block
+ * chunks without the doubled index on the wire. gcow_index_pack16_device builds it on the device from the index every
+ * 8 blocks of one stream of `field`'s shape (gcow_index_entries(field, 8) entries at d_index8) into
+ * gcow_index_entries(field, 16) entries at d_out. GCOW_ERR_UNSUPPORTED when p lets 8 blocks exceed 65535 bits
+ * (minbits > 8191) or the stream 2^48 bits; 1-D fields only.
+ */
+#define GCOW_INDEX_PACKED16 0x1010u
+gcow_status gcow_index_pack16_device(const zfp_input* field, const gcow_params* p, const uint64_t* d_index8,
+                                     uint64_t* d_out, void* hip_stream);
 
 /*
  * zfp 0.5.5 stream header: the byte format zfpy.compress_numpy writes (hw/models/train_imagenet.py:459-465 calls

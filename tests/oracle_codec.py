@@ -67,8 +67,24 @@ class OracleCodec:
             return out
         return t
 
+    def pack_index16(self, index8: torch.Tensor, n: int, params) -> torch.Tensor:
+        """include/gcow.h GCOW_INDEX_PACKED16, restated in numpy: entry c = idx8[2c] | (idx8[2c+1] - idx8[2c]) << 48."""
+        i8 = index8.numpy().view(np.uint64)[: (n + 31) // 32]
+        a = i8[0::2]
+        b = np.zeros_like(a)
+        b[: len(i8[1::2])] = i8[1::2] - a[: len(i8[1::2])]
+        assert b.max(initial=0) < 1 << 16 and a.max(initial=0) < 1 << 48
+        self.records.append(("pack_index16", n))
+        return torch.from_numpy((a | (b << np.uint64(48))).view(np.int64).copy())
+
     def decode_mean(self, streams: torch.Tensor, stream_words: int, nstreams: int, n: int, params, index=None,
                     index_words: int = 0, index_stride: int = 0, out=None):
+        if index is not None and index_stride == 0x1010:  # packed16: unpack to the 8-block chunk starts
+            pk = index.numpy().view(np.uint64).reshape(nstreams, index_words)
+            lo = pk & np.uint64((1 << 48) - 1)
+            un = np.stack([lo, lo + (pk >> np.uint64(48))], axis=2).reshape(nstreams, 2 * index_words)
+            index, index_words, index_stride = torch.from_numpy(un.view(np.int64).copy().reshape(-1)), \
+                2 * index_words, 8
         s = _u64(streams)
         p = _params(params)
         acc = np.zeros(n, np.float32)

@@ -92,6 +92,21 @@ MEAN_MODES = {"rate16": (16,), "rate8": (8,), "rate2.5": (2.5,), "expert_generic
               "expert_var_minbits": (8, 512, 32, -1074), "expert_var_trunc": (1, 100, 64, -30)}
 
 
+def _enc_stride(stride):
+    """The encoder's index spacing for a decode_mean index form: 8, 16, or "packed" (encoded every 8 blocks, sent as
+    the packed 16-block index, ddp.compressed_allgather_hook's form)."""
+    return 8 if stride == "packed" else stride
+
+
+def _mean_index(gc, encs, stride, n, p):
+    """(index tensor, entries per stream, decode_mean index_stride) of the encodes `encs` in the form `stride`."""
+    if stride == "packed":
+        pk = [gc.pack_index16(e.index, n, p) for e in encs]
+        return torch.cat(pk), pk[0].numel(), gc.INDEX_PACKED16
+    ni = encs[0].index.numel()
+    return torch.cat([e.index[:ni] for e in encs]), ni, stride
+
+
 def _mean_op(orc, mode):
     v = MEAN_MODES[mode]
     if isinstance(v, float):
@@ -101,25 +116,24 @@ def _mean_op(orc, mode):
 
 @pytest.mark.parametrize("mode", list(MEAN_MODES))
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-@pytest.mark.parametrize("stride", [16, 8])
+@pytest.mark.parametrize("stride", [16, 8, "packed"])
 def test_decode_mean_vs_oracle(gc, orc, mode, world, stride):
-    n = 4 * 20001 + 2  # a partial last block; > 128 index chunks
+    n = 4 * 20001 + 2  # a partial last block; > 128 index chunks; 5001 blocks: the last 16-block entry has no midpoint
     op = _mean_op(orc, mode)
     fixed = op.minbits == op.maxbits
     if fixed and stride != 16:
         pytest.skip("fixed rate takes no index")
     buckets = [_bucket(orc, n, 900 + r, mode.startswith("bf16")) for r in range(world)]
-    encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else stride) for b in buckets]
+    encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else _enc_stride(stride)) for b in buckets]
     lens = [e.bits for e in encs]
     sw = max((b + 63) // 64 for b in lens) + (0 if fixed else 1)
     streams = torch.zeros(world * sw + 2, dtype=torch.int64, device="cuda")
     for r, e in enumerate(encs):
         streams[r * sw:r * sw + e.nwords] = e.stream()
-    idx, ni = None, 0
+    idx, ni, st = None, 0, 0
     if not fixed:
-        ni = encs[0].index.numel()
-        idx = torch.cat([e.index[:ni] for e in encs])
-    got = gc.decode_mean(streams, sw, world, n, _P(gc, op), idx, ni, 0 if fixed else stride)
+        idx, ni, st = _mean_index(gc, encs, stride, n, _P(gc, op))
+    got = gc.decode_mean(streams, sw, world, n, _P(gc, op), idx, ni, st)
     want = _oracle_mean(orc, [orc.compress(b, op)[0] for b in buckets], op, n)
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
@@ -134,7 +148,7 @@ def _bf16_rne(a: np.ndarray) -> np.ndarray:
 @pytest.mark.parametrize("mode", list(MEAN_MODES))
 @pytest.mark.parametrize("world", [1, 3])
 @pytest.mark.parametrize("layout", ["contiguous", "strided"])
-@pytest.mark.parametrize("stride", [16, 8])
+@pytest.mark.parametrize("stride", [16, 8, "packed"])
 def test_decode_mean_bf16_output(gc, orc, mode, world, layout, stride):
     """decode_mean into a bf16 bucket (the hook's receive side for bf16 gradients): the fp32 mean of the oracle
     decodes, rounded to nearest even, written in place -- contiguous (8-byte block stores, the lean kernels' transposed
@@ -145,18 +159,17 @@ def test_decode_mean_bf16_output(gc, orc, mode, world, layout, stride):
     if fixed and stride != 16:
         pytest.skip("fixed rate takes no index")
     buckets = [_bucket(orc, n, 700 + r, mode.startswith("bf16")) for r in range(world)]
-    encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else stride) for b in buckets]
+    encs = [gc.encode(_dev(b), _P(gc, op), index_stride=0 if fixed else _enc_stride(stride)) for b in buckets]
     sw = max((e.bits + 63) // 64 for e in encs) + (0 if fixed else 1)
     streams = torch.zeros(world * sw + 2, dtype=torch.int64, device="cuda")
     for r, e in enumerate(encs):
         streams[r * sw:r * sw + e.nwords] = e.stream()
-    idx, ni = None, 0
+    idx, ni, st = None, 0, 0
     if not fixed:
-        ni = encs[0].index.numel()
-        idx = torch.cat([e.index[:ni] for e in encs])
+        idx, ni, st = _mean_index(gc, encs, stride, n, _P(gc, op))
     base = torch.full((2 * n,), -1.0, dtype=torch.bfloat16, device="cuda")
     out = base[:n] if layout == "contiguous" else base[::2]
-    got = gc.decode_mean(streams, sw, world, n, _P(gc, op), idx, ni, 0 if fixed else stride, out=out)
+    got = gc.decode_mean(streams, sw, world, n, _P(gc, op), idx, ni, st, out=out)
     want = _bf16_rne(_oracle_mean(orc, [orc.compress(b, op)[0] for b in buckets], op, n))
     torch.cuda.synchronize()
     assert got.data_ptr() == out.data_ptr()
@@ -167,14 +180,14 @@ def test_decode_mean_bf16_output(gc, orc, mode, world, layout, stride):
 
 @pytest.mark.parametrize("out_dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("stride", [16, 8])
+@pytest.mark.parametrize("stride", [16, 8, "packed"])
 def test_decode_mean_stage_parts(gc, orc, world, out_dtype, stride):
     """k_decode_mean1d_var_lean stages each stream's span of a workgroup (128 chunks of 16 blocks) in 1, 2 or 4 parts
     (a stage of 64 bits per block). Ranks hold data of very different magnitudes at accuracy 1e-6: N(0, 1e4) codes
     ~137 bits per block (every group in 4 parts), N(0, 1) ~100 (2 parts), N(0, 1e-3) ~64 (1 part, or 2); inside rank 0 the
     groups alternate between the first two. nchunks is a whole number of workgroups, so the last group's span runs to
     stream_words, far past the shorter ranks' streams. Bit-exact vs the oracle mean, fp32 and bf16 out."""
-    wg = 128 * stride * 4  # values per workgroup (128 chunks of `stride` blocks)
+    wg = 128 * _enc_stride(stride) * 4  # values per workgroup (128 chunks of `stride` blocks)
     n = wg * 7
     rng = np.random.default_rng(31337 + world)
     scales = [1e4, 1.0, 1e-3]
@@ -187,7 +200,7 @@ def test_decode_mean_stage_parts(gc, orc, world, out_dtype, stride):
         buckets.append(a)
     op = orc.accuracy(1e-6)
     p = _P(gc, op)
-    encs = [gc.encode(_dev(b), p, index_stride=stride) for b in buckets]
+    encs = [gc.encode(_dev(b), p, index_stride=_enc_stride(stride)) for b in buckets]
     lens = [e.bits for e in encs]
     bpb = [b / (n // 4) for b in lens]
     assert bpb[0] > 100 and (world < 2 or 80 < bpb[1] < 128) and (world < 3 or bpb[2] < 72), bpb
@@ -195,16 +208,15 @@ def test_decode_mean_stage_parts(gc, orc, world, out_dtype, stride):
     streams = torch.zeros(world * sw + 2, dtype=torch.int64, device="cuda")
     for r, e in enumerate(encs):
         streams[r * sw:r * sw + e.nwords] = e.stream()
-    ni = encs[0].index.numel()
-    idx = torch.cat([e.index[:ni] for e in encs])
+    idx, ni, st = _mean_index(gc, encs, stride, n, p)
     want = _oracle_mean(orc, [orc.compress(b, op)[0] for b in buckets], op, n)
     if out_dtype == "f32":
-        got = gc.decode_mean(streams, sw, world, n, p, idx, ni, stride)
+        got = gc.decode_mean(streams, sw, world, n, p, idx, ni, st)
         torch.cuda.synchronize()
         assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
     else:
         out = torch.empty(n, dtype=torch.bfloat16, device="cuda")
-        gc.decode_mean(streams, sw, world, n, p, idx, ni, stride, out=out)
+        gc.decode_mean(streams, sw, world, n, p, idx, ni, st, out=out)
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().view(torch.int16).numpy().view(np.uint16), _bf16_rne(want))
 
@@ -213,22 +225,23 @@ def test_decode_mean_stage_parts(gc, orc, world, out_dtype, stride):
 def test_decode_mean_full_size_w8(gc, orc, mode):
     """The hook's receive side at the bench's size: 8 streams of 256 Mi fp32 values (8 different buckets, the bench's
     fill_normal with seeds 0x67636F77 + r) decoded and averaged in one launch == the threaded oracle decodes summed
-    in rank order in fp32, divided by 8, over the whole bucket."""
+    in rank order in fp32, divided by 8, over the whole bucket. Variable rate with the all-gather hook's packed
+    16-block index (8-block chunks)."""
     W, n = 8, 256 * 1024 * 1024
     T = min(16, os.cpu_count() or 1)
     op = orc.rate(16, 1) if mode == "rate16" else orc.accuracy(1e-6)
     fixed = op.minbits == op.maxbits
     p = _P(gc, op)
     x = torch.empty(n, dtype=torch.float32, device="cuda")
-    enc = gc.Encoder((n,), torch.float32, p, index_stride=0 if fixed else 16)
+    enc = gc.Encoder((n,), torch.float32, p, index_stride=0 if fixed else 8)
     acc = np.zeros(n, np.float32)
     parts, idx = [], []
     for r in range(W):
         gc.fill_normal(x, 1e-3, seed=0x67636F77 + r, inject=True)
         e = enc(x)
         parts.append(e.stream().clone())
-        if not fixed:
-            idx.append(e.index.clone())
+        if not fixed:  # the all-gather hook's index: every 8 blocks, sent packed into the 16-block entries
+            idx.append(gc.pack_index16(e.index, n, p).clone())
         w_ref, bits, offs = orc.compress(x.cpu().numpy(), op, threads=T, offsets=True)
         assert e.bits == bits
         acc = acc + orc.decompress(w_ref, (n,), op, threads=T, offsets=None if fixed else offs)
@@ -240,9 +253,32 @@ def test_decode_mean_full_size_w8(gc, orc, mode):
     for r, s in enumerate(parts):
         streams[r * sw:r * sw + s.numel()] = s
     ni = idx[0].numel() if idx else 0
-    got = gc.decode_mean(streams, sw, W, n, p, torch.cat(idx) if idx else None, ni, 0 if fixed else 16, out=x)
+    got = gc.decode_mean(streams, sw, W, n, p, torch.cat(idx) if idx else None, ni, 0 if fixed else gc.INDEX_PACKED16,
+                         out=x)
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("nblocks", [1, 7, 8, 9, 16, 17, 24, 4096 + 9])
+def test_pack_index16(gc, orc, nblocks):
+    """gcow_index_pack16_device: entry c = idx8[2c] | (idx8[2c+1] - idx8[2c]) << 48, the offset 0 where block 16c + 8
+    does not exist; parameters that let 8 blocks pass 65535 bits, and 2-D fields, are refused."""
+    n = 4 * nblocks - 1
+    p = gc.accuracy(1e-6)
+    e = gc.encode(_dev(_bucket(orc, n, 11)), p, index_stride=8)
+    pk = gc.pack_index16(e.index, n, p).cpu().numpy().view(np.uint64)
+    i8 = e.index.cpu().numpy().view(np.uint64)[: (nblocks + 7) // 8]
+    a = i8[0::2]
+    d = np.zeros_like(a)
+    d[: i8[1::2].size] = i8[1::2] - a[: i8[1::2].size]
+    torch.cuda.synchronize()
+    assert pk.size == (nblocks + 15) // 16 and np.array_equal(pk, a | (d << np.uint64(48)))
+    with pytest.raises(gc.GcowError):
+        gc.pack_index16(e.index, n, gc.expert(8192, 16658, 64, -1074))
+    f2 = gc.field_of_shape((4, nblocks), torch.float32)
+    with pytest.raises(gc.GcowError):
+        gc.check(gc.load().gcow_index_pack16_device(gc.C.byref(f2), gc.C.byref(p), e.index.data_ptr(),
+                                                    e.index.data_ptr(), None), "pack")
 
 
 def test_decode_mean_argument_checks(gc, orc):
@@ -289,6 +325,9 @@ class HostStagedDeviceCodec:
     def decode(self, words, n, params, index=None, index_stride=0, out=None):
         o = self.d.decode(words.cuda(), n, params, index.cuda() if index is not None else None, index_stride).cpu()
         return out.copy_(o) if out is not None else o
+
+    def pack_index16(self, index8, n, params):
+        return self.d.pack_index16(index8.cuda(), n, params).cpu()
 
     def decode_mean(self, streams, stream_words, nstreams, n, params, index=None, index_words=0, index_stride=0,
                     out=None):
