@@ -715,19 +715,21 @@ def leg_decode_mean(ctx, W: int = 8, names=("rate16", "acc1e-6")):
         nip = ixp.numel() // W if stride else 0
         del parts, idx, enc
         kp = codec.INDEX_PACKED16 if stride else 0
-        _, per = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ixp, nip, kp, out=mean, stream=st), 3, 10,
-                       stream=st)
-        k = sum(per) / len(per)
-        k8 = k16 = None
+        forms = {"packed": lambda: codec.decode_mean(buf, sw, W, n, p, ixp, nip, kp, out=mean, stream=st)}
+        ix16 = None
         if stride:  # the same decode with the plain 8-block index, and with a plain 16-block index (16-block chunks)
-            _, per8 = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ix8, ni8, sstride, out=mean, stream=st), 3,
-                            10, stream=st)
-            k8 = round(sum(per8) / len(per8), 4)
             ix16 = ix8.view(W, ni8)[:, ::stride // sstride].contiguous().view(-1)
-            _, per16 = timed(ctx, lambda: codec.decode_mean(buf, sw, W, n, p, ix16, ix16.numel() // W, stride, out=mean,
-                                                            stream=st), 3, 10, stream=st)
-            k16 = round(sum(per16) / len(per16), 4)
-            del ix16
+            forms["8"] = lambda: codec.decode_mean(buf, sw, W, n, p, ix8, ni8, sstride, out=mean, stream=st)
+            forms["16"] = lambda: codec.decode_mean(buf, sw, W, n, p, ix16, ix16.numel() // W, stride, out=mean,
+                                                    stream=st)
+        kt = {f: [] for f in forms}
+        for _ in range(2):  # the forms interleaved (two rounds), so no form always meets the clock state of one slot
+            for f, fn in forms.items():
+                kt[f] += timed(ctx, fn, 3, 10, stream=st)[1]
+        k = sum(kt["packed"]) / len(kt["packed"])
+        k8 = round(sum(kt["8"]) / len(kt["8"]), 4) if stride else None
+        k16 = round(sum(kt["16"]) / len(kt["16"]), 4) if stride else None
+        del ix16
         kname = "k_decode_mean_fixed1d_np<64>" if stride == 0 else "k_decode_mean1d_var_lean<128, 64, 8, packed16>"
         # the sharded receive (ddp.compressed_sharded_hook): one rank's decode-mean of its 1/W shard from the W pieces
         # the all-to-all delivers (cut here from the same streams; the exchange itself is an N > 1 leg)
