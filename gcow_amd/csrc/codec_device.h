@@ -61,17 +61,39 @@ typedef unsigned int st_v4u __attribute__((ext_vector_type(4)));
 
 // nbytes (<= MAXC * 16) bytes from src (16-byte aligned) to dst[0 .. MAXC) as 16-byte chunks; chunks past nbytes read
 // zero (buffer range check), so every lane issues the same loads. T threads.
-template <uint32_t T, uint32_t MAXC>
+// SWZ: a stream span for lane-parallel bit reads -- chunk k goes to chunk slot k ^ ((k >> 4) & 15), i.e. qword q of
+// the span lives at lds_qword_swz(q): each 256-byte bank row's qword pairs XOR-permuted by the row index, so lanes
+// reading chunk starts spaced a multiple of ~32 qwords apart (8- or 16-block chunks at any bit rate) land on
+// different banks.
+#ifndef GCOW_SWZ_OPAQUE_ZERO
+#define GCOW_SWZ_OPAQUE_ZERO 0  // measurement builds: the same instructions with an identity mapping (an opaque 0 mask)
+#endif
+__device__ __forceinline__ uint32_t swz_mask(uint32_t m)
+{
+  if constexpr (GCOW_SWZ_OPAQUE_ZERO) {
+    uint32_t z = 0;
+    asm volatile("" : "+v"(z));
+    return m & z;
+  }
+  return m;
+}
+__device__ __forceinline__ uint32_t lds_qword_swz(uint32_t q) { return q ^ ((q >> 4) & swz_mask(30u)); }
+
+template <uint32_t T, uint32_t MAXC, bool SWZ = false>
 __device__ __forceinline__ void stage_lds16(void* dst, const void* src, uint32_t nbytes)
 {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(src), 0, (int)nbytes, 0x00020000);
   constexpr uint32_t R = (MAXC + T - 1) / T;
+  // the swizzle permutes chunks within groups of 16: a partial last group must be one the swizzle leaves in place
+  static_assert(!SWZ || MAXC % 16 == 0 || ((MAXC >> 4) & 15u) == 0, "swizzled chunks stay inside the stage");
   st_v4u v[R];
 #pragma unroll
   for (uint32_t i = 0; i < R; i++) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((threadIdx.x + T * i) * 16u), 0, 0);
 #pragma unroll
-  for (uint32_t i = 0; i < R; i++)
-    if (MAXC % T == 0 || threadIdx.x + T * i < MAXC) ((st_v4u*)dst)[threadIdx.x + T * i] = v[i];
+  for (uint32_t i = 0; i < R; i++) {
+    const uint32_t k = threadIdx.x + T * i;
+    if (MAXC % T == 0 || k < MAXC) ((st_v4u*)dst)[SWZ ? k ^ ((k >> 4) & swz_mask(15u)) : k] = v[i];
+  }
 }
 
 // A constant table of N 32-bit words (N * 4 a multiple of 16) into LDS.

@@ -1736,6 +1736,17 @@ struct LdsWindow {
   }
 };
 
+// The same over a span staged with stage_lds16<.., SWZ = true> (qword q at lds_qword_swz(q)).
+struct LdsWindowSwz {
+  const uint64_t* w;
+  __device__ __forceinline__ uint64_t operator()(uint64_t pos) const
+  {
+    const uint32_t i = (uint32_t)(pos >> 6), sh = (uint32_t)(pos & 63);
+    const uint64_t lo = w[lds_qword_swz(i)] >> sh;
+    return sh ? lo | (w[lds_qword_swz(i + 1)] << (64 - sh)) : lo;
+  }
+};
+
 // dtab: the full (n, r, 7 bits) plane table, or (COMPACT) its r = 7 rows only, indexed (n, 7 bits)
 template <class Win, bool COMPACT = true>
 __device__ __forceinline__ void decode_block1d_var(const Win& win, uint64_t& pos, const uint16_t* dtab, int minexp,
@@ -1862,8 +1873,16 @@ __global__ __launch_bounds__(256) void k_decode1d_var(FieldDesc F, Params p, con
 //    are coded (accuracy 1e-6 on gradient-scale data codes ~14).
 // Positions are 32-bit, relative to the staged words (LDS), and windows are built from three 32-bit words with two
 // v_alignbit_b32.
+template <bool SWZ = false>
 __device__ __forceinline__ uint64_t lds_win64(const uint32_t* w, uint32_t pos)
 {
+  if constexpr (SWZ) {  // two aligned qword reads of the swizzled span (ds_read_b64: 64 banks), three words selected
+    const uint32_t q = pos >> 6;
+    const uint2 lo = ((const uint2*)w)[lds_qword_swz(q)], hi = ((const uint2*)w)[lds_qword_swz(q + 1)];
+    const bool up = (pos & 32u) != 0;
+    const uint32_t a = up ? lo.y : lo.x, b = up ? hi.x : lo.y, c = up ? hi.y : hi.x;
+    return ((uint64_t)__builtin_amdgcn_alignbit(c, b, pos) << 32) | __builtin_amdgcn_alignbit(b, a, pos);
+  }
   const uint32_t i = pos >> 5;
   const uint32_t a = w[i], b = w[i + 1], c = w[i + 2];
   return ((uint64_t)__builtin_amdgcn_alignbit(c, b, pos) << 32) | __builtin_amdgcn_alignbit(b, a, pos);
@@ -1871,11 +1890,11 @@ __device__ __forceinline__ uint64_t lds_win64(const uint32_t* w, uint32_t pos)
 
 // returns false when the block needs the general decoder (pos unchanged then). PAIR: tab is the DecTabLP image and
 // the group phase decodes up to two planes per lookup; else tab is DecTab7.
-template <bool PAIR = false>
+template <bool PAIR = false, bool SWZ = false>
 __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& pos, const uint16_t* tab, int cexp,
                                                  int maxprec, float* f)
 {
-  const uint64_t w = lds_win64(sw, pos);
+  const uint64_t w = lds_win64<SWZ>(sw, pos);
   const int emax = (int)((w >> 1) & 255u) - 127;
   const int np = min(32, min(maxprec, max(0, emax + cexp)));  // coded planes 31 .. 32 - np
   // empty planes: ctz of the 55 bits after the header, a sentinel one at bit 55 for none (any np <= 32 < 55)
@@ -1903,7 +1922,7 @@ __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& p
     while (n < 3 && j < lim) {
       if (off > 54u) {
         wbase += off;
-        gw = lds_win64(sw, wbase);
+        gw = lds_win64<SWZ>(sw, wbase);
         off = 0;
       }
       const uint32_t b = (uint32_t)(gw >> off) & 1023u;
@@ -1926,7 +1945,7 @@ __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& p
     while (n < 3 && j < nbelow && j < 8) {
       if (off > 57u) {
         wbase += off;
-        gw = lds_win64(sw, wbase);
+        gw = lds_win64<SWZ>(sw, wbase);
         off = 0;
       }
       const uint32_t e = dt7[(n << 7) | ((uint32_t)(gw >> off) & 127u)];
@@ -1942,8 +1961,8 @@ __device__ __forceinline__ bool dec_block1d_lean(const uint32_t* sw, uint32_t& p
   const uint32_t nb = 4u * t;                 // <= 128
   // the run's window is not masked at nb: the next block's bits beyond it land on planes below kmin = 32 - np, which
   // one mask of the coefficients clears
-  uint64_t v0 = lds_win64(sw, vpos), v1 = 0;
-  if (nb > 64) v1 = lds_win64(sw, vpos + 64);
+  uint64_t v0 = lds_win64<SWZ>(sw, vpos), v1 = 0;
+  if (nb > 64) v1 = lds_win64<SWZ>(sw, vpos + 64);
   const uint32_t sft = 4u * (uint32_t)j;  // <= 32
   const uint64_t Ylo = (uint64_t)G | (v0 << sft);
   uint32_t u[4] = {0u, 0u, 0u, 0u};
@@ -2018,6 +2037,9 @@ __device__ __forceinline__ void xpose8_stage(float (&g)[8][4], uint32_t lane)
 #ifndef GCOW_VDEC_BIGB
 #define GCOW_VDEC_BIGB 144
 #endif
+#ifndef GCOW_VDEC_SWZ
+#define GCOW_VDEC_SWZ 0  // the staged spans XOR-swizzled by bank row (lds_qword_swz), windows by qword reads
+#endif
 // Stage capacity in stream words: the main kernel's (GCOW_VDEC_CAPB bits per block on average) and the second pass's
 // (any span: a 1-D block codes at most 140 bits, plus the 16-byte alignment of the span's start)
 template <uint32_t LANES, uint32_t CAPB = GCOW_VDEC_CAPB> constexpr uint32_t vdec_cap() { return LANES * 16 * CAPB / 64; }
@@ -2058,7 +2080,8 @@ __device__ __forceinline__ void vdec_group(const FieldDesc& F, const Params& p, 
   if constexpr (BIG) __syncthreads();
   else if constexpr (LP) stage_lds16<LANES, sizeof(DecTabLP) / 16>(dtab, &g_dec_lean_pair, sizeof(DecTabLP));
   else stage_lds16<LANES, sizeof(DecTab7) / 16>(dt7, &g_dec_tab7, sizeof(DecTab7));
-  if (staged) stage_lds16<LANES, (CAP + 4) / 2>(sw, in + w0, (uint32_t)(8 * span));
+  constexpr bool SWZ = GCOW_VDEC_SWZ;
+  if (staged) stage_lds16<LANES, (CAP + 4) / 2, SWZ>(sw, in + w0, (uint32_t)(8 * span));
   __syncthreads();
   float* out = (float*)F.data;
   const bool whole = c0 + LANES <= nchunks && 16 * (c0 + LANES) <= (uint64_t)F.n[0] / 4;  // no partial chunk or block
@@ -2070,7 +2093,8 @@ __device__ __forceinline__ void vdec_group(const FieldDesc& F, const Params& p, 
       pos -= 64 * w0;
       for (uint64_t b = b0; b < b1; b++) {
         float f[4];
-        decode_block1d_var(LdsWindow{sw}, pos, dt7, p.minexp, p.maxprec, f);
+        if constexpr (SWZ) decode_block1d_var(LdsWindowSwz{sw}, pos, dt7, p.minexp, p.maxprec, f);
+        else decode_block1d_var(LdsWindow{sw}, pos, dt7, p.minexp, p.maxprec, f);
         store_block1d(F, b, f);
       }
       pos += 64 * w0;
@@ -2097,9 +2121,10 @@ __device__ __forceinline__ void vdec_group(const FieldDesc& F, const Params& p, 
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const uint32_t start = pos;
-      if (!dec_block1d_lean<LP>(sw32, pos, dtab, cexp, maxprec, g[k])) {
+      if (!dec_block1d_lean<LP, SWZ>(sw32, pos, dtab, cexp, maxprec, g[k])) {
         uint64_t p64 = start;
-        decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, g[k]);
+        if constexpr (SWZ) decode_block1d_var(LdsWindowSwz{sw}, p64, dt7, p.minexp, p.maxprec, g[k]);
+        else decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, g[k]);
         pos = (uint32_t)p64;
       }
     }
@@ -2570,6 +2595,9 @@ __global__ __launch_bounds__(256) void k_decode_mean_fixed1d_np(FieldDesc F, Par
 #ifndef GCOW_DMV16_LPAIR
 #define GCOW_DMV16_LPAIR 1  // 16-block chunks too, at 3 waves (LDS): 3.67 -> 3.59 ms (profiles/r05_dmean16_lp_w3_ab.log)
 #endif
+#ifndef GCOW_DMV_SWZ
+#define GCOW_DMV_SWZ 0  // decode_mean's staged spans XOR-swizzled by bank row (lds_qword_swz), windows by qword reads
+#endif
 #ifndef GCOW_DMV_LPAIR
 #define GCOW_DMV_LPAIR 1  // the lean block decoder's group phase through the 16-bit pair table (DecTabLP)
 #endif
@@ -2638,7 +2666,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(CH == 8 ?
       const int64_t w0 = w_first(a);
       const uint64_t span = (uint64_t)(w_end(a + per) - w0);
       __syncthreads();  // the previous span is no longer read
-      stage_lds16<LANES, (CAP + 4) / 2>(sw, sr + w0, (uint32_t)(8 * span));
+      stage_lds16<LANES, (CAP + 4) / 2, GCOW_DMV_SWZ>(sw, sr + w0, (uint32_t)(8 * span));
       __syncthreads();
       if (tid / per != part) continue;
       uint32_t pos = (uint32_t)((int64_t)mine - 64 * w0);
@@ -2646,9 +2674,10 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(CH == 8 ?
       for (int k = 0; k < (int)CH; k++) {
         const uint32_t start = pos;
         float f[4];
-        if (!dec_block1d_lean<LP>(sw32, pos, dtab, cexp, maxprec, f)) {
+        if (!dec_block1d_lean<LP, GCOW_DMV_SWZ>(sw32, pos, dtab, cexp, maxprec, f)) {
           uint64_t p64 = start;
-          decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, f);
+          if constexpr (GCOW_DMV_SWZ) decode_block1d_var(LdsWindowSwz{sw}, p64, dt7, p.minexp, p.maxprec, f);
+          else decode_block1d_var(LdsWindow{sw}, p64, dt7, p.minexp, p.maxprec, f);
           pos = (uint32_t)p64;
         }
 #pragma unroll
@@ -2947,7 +2976,11 @@ static void launch_fixed1d_t(const void* in, uint64_t nvals, const Params& p, vo
 #define GCOW_C2_U 8  // A/B builds only (tools/build_variant.sh -DGCOW_C2_U=4)
 #endif
         constexpr int U = GCOW_C2_U;
-        k_encode_fixed1d_np<DT, WB, U, 256, 3><<<(nc + 256 * U - 1) / (256 * U), 256, 0, st>>>(ic, nc, p, oc);
+#ifndef GCOW_C2_LDS_PAD
+#define GCOW_C2_LDS_PAD 0  // A/B builds only: unused dynamic LDS per workgroup, i.e. fewer workgroups per CU
+#endif
+        k_encode_fixed1d_np<DT, WB, U, 256, 3><<<(nc + 256 * U - 1) / (256 * U), 256, GCOW_C2_LDS_PAD, st>>>(ic, nc, p,
+                                                                                                          oc);
       }
     }
   }

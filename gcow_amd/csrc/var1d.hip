@@ -43,7 +43,8 @@ constexpr uint64_t V1VAL = (1ull << 62) - 1;                 // status word: fla
 // V1_ABLATE (measurement builds only, tools/ubench/var1d_ablate.sh; 0 in the product): 1 = no look-back (tile t at
 // t * 64 Ki bits), 2 = no coding (zero codes / prepared words, lengths kept), 4 = no window store, 8 = no pair loop,
 // 16 = no prepare in the tile coder (raw words as coefficients), 32 = no length computation in the tile count,
-// 64 = no input / length loads in the tile coder (synthetic words, 58-bit blocks)
+// 64 = no input / length loads in the tile coder (synthetic words, 58-bit blocks), 128 = no LDS window writes in the
+// tile coder (the accumulator words folded into one register), 256 = no spread-table window lookups in the coder
 #ifndef V1_ABLATE
 #define V1_ABLATE 0
 #endif
@@ -137,7 +138,8 @@ __device__ __forceinline__ void v1_code(const uint32_t* u, uint32_t hdr, uint32_
   // group phase: window nibbles 0 .. jg, of which planes >= kmin are coded (nibbles <= K - sh)
   const int jg = (int)min(ffbh_hw(S2), K) - (int)sh;
   const uint32_t w0 = u[0] << sh, w1 = u[1] << sh, w2 = u[2] << sh, w3 = u[3] << sh;
-  const uint64_t Y = window_lds(rs, w0, w1, w2, w3);  // planes M0 .. M0 - 15 as nibbles
+  const uint64_t Y = (V1_ABLATE & 256) ? (((uint64_t)(w0 ^ w1) << 32) | (w2 ^ w3))
+                                        : window_lds(rs, w0, w1, w2, w3);  // planes M0 .. M0 - 15 as nibbles
   const uint32_t pos0 = 9u + sh;                      // header + one '0' per empty plane
   uint32_t e = tab[(uint32_t)Y & 255u];
   uint64_t G = e >> 17;
@@ -156,7 +158,8 @@ __device__ __forceinline__ void v1_code(const uint32_t* u, uint32_t hdr, uint32_
   const uint32_t vs = 4u * jl - 8u;  // 0 .. 56: V = W >> (vs + 8)
   uint64_t V0 = (Y >> 8) >> vs, V1 = 0;
   if (__any(M0 >= 16 && pos0 + gl + 56u - vs < len)) {  // plane M0 - 16 lands at pos0 + gl + 4 (16 - jl)
-    const uint64_t Y2 = window_lds_low(rs, w0, w1, w2, w3);
+    const uint64_t Y2 = (V1_ABLATE & 256) ? (((uint64_t)(w0 + w1) << 32) | (w2 + w3))
+                                          : window_lds_low(rs, w0, w1, w2, w3);
     V0 |= Y2 << (56u - vs);
     V1 = (Y2 >> 8) >> vs;
   }
@@ -750,6 +753,7 @@ __device__ __forceinline__ void v1_tile_code(const FieldDesc& F, const Params& p
   uint32_t q = excl >> 6, fill = excl & 63u;
   const uint32_t qhead = q;
   uint32_t spmask = 0;
+  [[maybe_unused]] uint64_t sink = 0;
 #pragma unroll
   for (uint32_t k = 0; k < V1U; k++) {
     float f[4];
@@ -781,16 +785,19 @@ __device__ __forceinline__ void v1_tile_code(const FieldDesc& F, const Params& p
     const uint64_t hi = (c1 >> 1) >> (63u - fill);
     const uint32_t nf = fill + len[k];
     if (nf >= 64u) {
-      if (q == qhead) atomicOr((unsigned long long*)&win[q], (unsigned long long)acc);
+      if constexpr ((V1_ABLATE & 128) != 0) sink ^= acc;
+      else if (q == qhead) atomicOr((unsigned long long*)&win[q], (unsigned long long)acc);
       else win[q] = acc;
       q++;
       acc = mid;
       if (nf >= 128u) {
-        win[q] = acc;
+        if constexpr ((V1_ABLATE & 128) != 0) sink ^= acc;
+        else win[q] = acc;
         q++;
         acc = hi;
         if (nf >= 192u) {  // a special block of up to 140 bits (its code is zero here) completes a third word
-          win[q] = acc;
+          if constexpr ((V1_ABLATE & 128) != 0) sink ^= acc;
+          else win[q] = acc;
           q++;
           acc = 0ull;
         }
@@ -799,7 +806,8 @@ __device__ __forceinline__ void v1_tile_code(const FieldDesc& F, const Params& p
     fill = nf & 63u;
     acc &= (1ull << fill) - 1ull;
   }
-  if (fill) atomicOr((unsigned long long*)&win[q], (unsigned long long)acc);
+  if constexpr ((V1_ABLATE & 128) != 0) win[qhead] = sink ^ acc;  // keeps the code alive
+  else if (fill) atomicOr((unsigned long long*)&win[q], (unsigned long long)acc);
   if (spmask) *s_special = 1u;
   __syncthreads();
   if (*s_special) {  // Inf / NaN blocks, long group phases, codes past 128 bits: the generic coder
