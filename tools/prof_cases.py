@@ -78,18 +78,23 @@ def vdec(reps):
 
 def dmean(reps, W=8):
     """decode_mean over W streams of 256 Mi values: rate 16, then accuracy 1e-6 with the block index every 16 and
-    every 8 blocks (the all-gather and the sharded hook's spacing)."""
+    every 8 blocks (the sharded hook's spacing), and every 8 blocks sent packed into 16-block entries (the all-gather
+    hook's form, codec.pack_index16)."""
     n = 256 << 20
     x = torch.empty(n, dtype=torch.float32, device="cuda")
     out = torch.empty_like(x)
-    for p, stride in ((codec.rate(16, 1), 0), (codec.accuracy(1e-6), 16), (codec.accuracy(1e-6), 8)):
-        enc = codec.Encoder((n,), torch.float32, p, index_stride=stride)
+    for p, stride in ((codec.rate(16, 1), 0), (codec.accuracy(1e-6), 16), (codec.accuracy(1e-6), 8),
+                      (codec.accuracy(1e-6), codec.INDEX_PACKED16)):
+        enc = codec.Encoder((n,), torch.float32, p, index_stride=8 if stride == codec.INDEX_PACKED16 else stride)
         ss, ix = [], []
         for r in range(W):
             codec.fill_normal(x, 1e-3, seed=0x67636F77 + r)
             e = enc(x)
             ss.append(e.stream().clone())
-            ix.append(e.index.clone() if stride else None)
+            if stride == codec.INDEX_PACKED16:
+                ix.append(codec.pack_index16(e.index, n, p).clone())
+            else:
+                ix.append(e.index.clone() if stride else None)
         sw = max(s.numel() for s in ss)
         buf = torch.zeros(W * sw + 2, dtype=torch.int64, device="cuda")
         for r, s in enumerate(ss):
