@@ -2049,15 +2049,34 @@ template <uint32_t LANES> constexpr uint32_t vdec_cap_big() { return LANES * 16 
 // whole (no partial chunk or block) with a contiguous output: left by the main kernel to k_decode1d_var_lean_big.
 // Not the last group: its span ends at the stream's end, which the index does not give (the buffer's end bounds it),
 // so it takes the main kernel's general path.
-template <uint32_t LANES, uint32_t CAPB>
-__device__ __forceinline__ bool vdec_left_to_big(const FieldDesc& F, const uint64_t* index, uint64_t in_words,
-                                                 uint64_t nchunks, uint64_t base_bits, uint64_t c0)
+template <uint32_t LANES>
+__device__ __forceinline__ bool vdec_left_to_big_w(const FieldDesc& F, const uint64_t* index, uint64_t in_words,
+                                                   uint64_t nchunks, uint64_t base_bits, uint64_t c0, uint64_t capw)
 {
   const bool whole = c0 + LANES < nchunks && 16 * (c0 + LANES) <= (uint64_t)F.n[0] / 4;
   if (!whole || !F.vec) return false;
   const uint64_t w0 = ((base_bits + index[c0]) >> 6) & ~1ull;
   const uint64_t wend = (base_bits + index[c0 + LANES] + 63) >> 6;
-  return min<uint64_t>(wend, in_words) - w0 > vdec_cap<LANES, CAPB>();
+  return min<uint64_t>(wend, in_words) - w0 > capw;
+}
+
+template <uint32_t LANES, uint32_t CAPB>
+__device__ __forceinline__ bool vdec_left_to_big(const FieldDesc& F, const uint64_t* index, uint64_t in_words,
+                                                 uint64_t nchunks, uint64_t base_bits, uint64_t c0)
+{
+  return vdec_left_to_big_w<LANES>(F, index, in_words, nchunks, base_bits, c0, vdec_cap<LANES, CAPB>());
+}
+
+// The stage tier of a stream from its block index (1: the 32-bit-per-block stage, 3: the 64-bit one): 1 when the
+// 32-bit stage holds 1.25 x the stream's average bits per block over chunks 0 .. nchunks - 2 -- the rule the launcher
+// applies to an exact-length buffer, taken here on the device for a buffer whose size says nothing (a capacity-sized
+// Encoder.words). The two tiers are launched gated; the workgroups of the one that does not match return after two
+// index loads (~13 us for the whole empty launch; a 48-bit tier measured as a second empty launch and was dropped).
+__device__ __forceinline__ uint32_t vdec_tier(const uint64_t* index, uint64_t nchunks)
+{
+  if (nchunks < 2) return 1;
+  const uint64_t span = index[nchunks - 1] - index[0], nbk = (nchunks - 1) * 16;
+  return span * 5 <= nbk * 32 * 4 ? 1u : 3u;
 }
 
 // One group: its span staged in sw (CAP words), each lane's 16 blocks decoded by the lean block decoder, stored
@@ -2148,11 +2167,12 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean(FieldDesc F, Params
                                                              uint64_t in_words, const uint64_t* __restrict__ index,
                                                              uint64_t nchunks, uint64_t base_bits,
                                                              uint64_t* __restrict__ end_out, uint64_t* __restrict__ left,
-                                                             uint64_t seq)
+                                                             uint64_t seq, uint32_t tier)
 {
   constexpr bool LP = GCOW_VDEC_LPAIR;
   __shared__ __attribute__((aligned(16))) uint16_t dtab[LP ? 3 * 1024 + 5 * 128 : 5 * 128];
   __shared__ __attribute__((aligned(16))) uint64_t sw[vdec_cap<LANES, CAPB>() + 4];
+  if (tier && vdec_tier(index, nchunks) != tier) return;  // gated: another tier's launch decodes this stream
   const uint64_t c0 = (uint64_t)blockIdx.x * LANES;
   if (vdec_left_to_big<LANES, CAPB>(F, index, in_words, nchunks, base_bits, c0)) {  // workgroup-uniform
     if (left && threadIdx.x == 0) atomicMax((unsigned long long*)left, (unsigned long long)seq);  // second pass has work
@@ -2175,13 +2195,20 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean_big(FieldDesc F, Pa
                                                                  uint64_t in_words, const uint64_t* __restrict__ index,
                                                                  uint64_t nchunks, uint64_t base_bits,
                                                                  uint64_t* __restrict__ end_out,
-                                                                 const uint64_t* __restrict__ left, uint64_t seq)
+                                                                 const uint64_t* __restrict__ left, uint64_t seq,
+                                                                 bool tiered)
 {
   __shared__ __attribute__((aligned(16))) uint16_t dt7[5 * 128];
   __shared__ __attribute__((aligned(16))) uint64_t sw[vdec_cap_big<LANES>() + 4];
   __shared__ uint32_t todo[LANES];
   __shared__ uint32_t ntodo;
   if (left && *left < seq) return;  // the main kernel left nothing (no flag word: check every group)
+  // the stage of the main launch that decoded this stream: CAPB, or (tiered) the tier vdec_tier picks
+  uint64_t capw = vdec_cap<LANES, CAPB>();
+  if (tiered) {
+    const uint32_t t = vdec_tier(index, nchunks);
+    capw = t == 1 ? vdec_cap<LANES, 32>() : vdec_cap<LANES, 64>();
+  }
   const uint64_t ng = (nchunks + LANES - 1) / LANES;
   bool staged_tab = false;
   // sweep k: workgroup w checks groups k G LANES + t G + w (t < LANES, G = gridDim.x): the groups spread over every
@@ -2191,7 +2218,7 @@ __global__ __launch_bounds__(LANES) void k_decode1d_var_lean_big(FieldDesc F, Pa
     if (threadIdx.x == 0) ntodo = 0;
     __syncthreads();
     const uint64_t g = gb + (uint64_t)threadIdx.x * G + blockIdx.x;
-    if (g < ng && vdec_left_to_big<LANES, CAPB>(F, index, in_words, nchunks, base_bits, g * LANES))
+    if (g < ng && vdec_left_to_big_w<LANES>(F, index, in_words, nchunks, base_bits, g * LANES, capw))
       todo[atomicAdd(&ntodo, 1u)] = threadIdx.x;
     __syncthreads();
     const uint32_t nt = ntodo;
@@ -3165,21 +3192,32 @@ hipError_t launch_decode1d_var(const FieldDesc& F, const Params& p, const uint64
     // The buffer is the caller's: a capacity-sized one (Encoder.words) reads as dense and keeps 64.
     const uint64_t nb = F.nblocks ? F.nblocks : 1, avail = in_words * 64 - std::min<uint64_t>(base_bits, in_words * 64);
     const uint32_t gbig = (uint32_t)std::min<uint64_t>(ng, 1024);
-    if (GCOW_VDEC_ADAPT && avail * 5 <= nb * 32 * 4) {
+    if (GCOW_VDEC_ADAPT && avail >= nb * 128) {
+      // a buffer of (near) the encoder's capacity (140 bits per block) says nothing about the stream: the 32- and
+      // 64-bit stage tiers launched gated on the stream's own average from its index (vdec_tier), the one that does not
+      // match returning after two index loads per workgroup (accuracy 1e-3 in a capacity buffer: 0.42 -> 0.37 ms;
+      // 1e-6: +13 us for the empty tier, profiles/r06_vdec_capacity_tiers.log)
       k_decode1d_var_lean<L, 32><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out,
-                                                             left, seq);
+                                                             left, seq, 1u);
+      k_decode1d_var_lean<L, 64><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out,
+                                                             left, seq, 3u);
+      k_decode1d_var_lean_big<L, 64><<<gbig, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left,
+                                                         seq, true);
+    } else if (GCOW_VDEC_ADAPT && avail * 5 <= nb * 32 * 4) {
+      k_decode1d_var_lean<L, 32><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out,
+                                                             left, seq, 0u);
       k_decode1d_var_lean_big<L, 32><<<gbig, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left,
-                                                         seq);
+                                                         seq, false);
     } else if (GCOW_VDEC_ADAPT && avail * 5 <= nb * 48 * 4) {
       k_decode1d_var_lean<L, 48><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out,
-                                                             left, seq);
+                                                             left, seq, 0u);
       k_decode1d_var_lean_big<L, 48><<<gbig, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits, end_out, left,
-                                                         seq);
+                                                         seq, false);
     } else {
       k_decode1d_var_lean<L, GCOW_VDEC_CAPB><<<(uint32_t)ng, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits,
-                                                                         end_out, left, seq);
+                                                                         end_out, left, seq, 0u);
       k_decode1d_var_lean_big<L, GCOW_VDEC_CAPB><<<gbig, L, 0, st>>>(F, p, in, in_words, index, nchunks, base_bits,
-                                                                     end_out, left, seq);
+                                                                     end_out, left, seq, false);
     }
     return hipGetLastError();
   }

@@ -185,6 +185,27 @@ def test_var1d_decode_exact_stream_buffer(gc, orc, tol, mix):
     assert np.array_equal(got.cpu().numpy().view(np.uint32), ref.view(np.uint32)), e.bits / ((n + 3) // 4)
 
 
+@pytest.mark.parametrize("tol,mix", [(1e-1, False), (1e-2, False), (1e-3, False), (1e-3, True), (1e-4, True),
+                                     (1e-6, False), (1e-6, True), (1e-9, False)])
+def test_var1d_decode_capacity_buffer_tiers(gc, orc, tol, mix):
+    """The same streams decoded from the encoder's capacity-sized buffer (what a hook holds): the buffer's size says
+    nothing about the stream, so launch_decode1d_var launches the 32 / 48 / 64-bit stage tiers gated on the stream's
+    average from its own index (vdec_tier) and the second pass takes the chosen tier's overflow. Bit for bit against
+    the oracle, sparse (1e-1: ~10 bits per block) to dense (1e-9: past every stage)."""
+    n = 4 * 16 * 128 * 9 + 4 * 16 * 37 + 4 * 5 + 2
+    a = orc.gen_normal(n, 1e-3, 0xCA9AC + int(-np.log10(tol)), True)
+    if mix:
+        a[: n // 2] *= np.float32(1e-3)
+        a[n // 2 + n // 8: n // 2 + n // 4] *= np.float32(30.0)
+    op = orc.accuracy(tol)
+    e, _ = dev_encode_bytes(gc, a, P(gc, op), 16)
+    assert e.words.numel() * 64 >= 128 * ((n + 3) // 4)  # the capacity buffer: the tiered launch
+    ref = orc.decompress(orc.compress(a, op)[0], a.shape, op)
+    got = gc.decode(e)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), ref.view(np.uint32)), e.bits / ((n + 3) // 4)
+
+
 def test_decode_bf16_output_needs_1d(gc, orc):
     a = orc.gen_normal(16 * 16, 1e-3, 5, False).reshape(16, 16)
     e, _ = dev_encode_bytes(gc, a, gc.rate(16, 2))
