@@ -34,7 +34,10 @@
 
 namespace gcow {
 
-constexpr uint32_t V1T = 256;                                // lanes per workgroup
+#ifndef GCOW_V1T
+#define GCOW_V1T 256
+#endif
+constexpr uint32_t V1T = GCOW_V1T;                           // lanes per workgroup
 constexpr uint32_t V1U = 4;                                  // consecutive blocks per lane
 constexpr uint32_t V1TILE = V1T * V1U;                       // blocks per tile
 constexpr uint32_t V1MAXB = 140;                             // 9 + 3 + 4 * 32: the longest 1-D block
@@ -559,7 +562,7 @@ constexpr uint32_t V1CT = 8;                                      // tiles per c
 #ifndef V1_COUNT_PF
 #define V1_COUNT_PF 1  // tiles of loads in flight ahead of the counted one (k_count1d_var_tile), 1 .. 3
 #endif
-constexpr uint32_t V1QS = 1500;                                   // small window, qwords
+constexpr uint32_t V1QS = 1500 * (V1T / 256);                     // small window, qwords (95 bits per block)
 constexpr uint32_t V1TAB = 1024;                                  // pair-table rows 0..3 in LDS
 
 // Raw buffer loads issued from inline asm, invisible to the compiler's waitcnt pass, with hand-counted waits (the
