@@ -17,6 +17,14 @@ namespace gcow {
 // bit offset -- before the budget check stops the lane.
 constexpr uint32_t E3_SLACK = 8;
 
+// occupancy bounds of the 3-D fixed-rate kernels (waves per SIMD; A/B knobs, the defaults are the measured best)
+#ifndef GCOW_E3F_WAVES
+#define GCOW_E3F_WAVES 4
+#endif
+#ifndef GCOW_D3F_WAVES
+#define GCOW_D3F_WAVES 6
+#endif
+
 
 // ------------------------------------------------------------------------------------------------ 3-D fixed rate
 // Fixed-rate 3-D blocks whose budget is a whole number of 32-bit words (maxbits = 32 WPB; rates 1, 2, 4, 8, 16, 32):
@@ -27,7 +35,7 @@ constexpr uint32_t E3_SLACK = 8;
 // kernels spills in their hot loop (C3 accuracy 1e-3: 0.591 -> 0.829 ms), so they are left alone
 // (profiles/r02_c3_occupancy_ab.log).
 template <int DT, uint32_t WPB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_encode3d_fixed(FieldDesc F, Params p, uint32_t* __restrict__ out32)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCOW_E3F_WAVES, 8))) void k_encode3d_fixed(FieldDesc F, Params p, uint32_t* __restrict__ out32)
 {
   constexpr uint32_t STRIDE = WPB + E3_SLACK + 1;  // odd: lanes' words spread over the banks
   extern __shared__ uint32_t lds_w[];               // 256 x STRIDE words, then the E table
@@ -194,7 +202,7 @@ __global__ __launch_bounds__(64) void k_encode3d_var(FieldDesc F, Params p, cons
 // group-test loops, and the extra waves hide more of it than the spills cost (C3 rate 8 decode 0.337 -> 0.297 ms,
 // tools/bench_configs.py c3).
 template <uint32_t WPB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_decode3d_fixed(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCOW_D3F_WAVES, 8))) void k_decode3d_fixed(
     FieldDesc F, Params p, const uint32_t* __restrict__ in32)
 {
   extern __shared__ uint32_t lds_w[];  // 256 x (WPB + 2) words: the block, then two zero pad words for peek64
